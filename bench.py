@@ -1,0 +1,179 @@
+"""Throughput bench of the north-star path: res15 eval forward over synthetic
+[B,101,40] fp32 MFCC maps resident in HBM, on the gfx950 kernels.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+One step = one forward of B clips per GPU (weak scaling: per-GPU batch fixed;
+the batch shards across ranks with no collective on the data path).  Prints ONE
+JSON line on rank 0 (see DESIGN.md "Measurement").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "1s-clips/sec (whole node) + top-1 acc, res15 12-label Speech Commands"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak (= FP32 vector peak)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--batch", type=int, default=131072, help="clips per GPU per step (C4: 1M over 8 GPUs)")
+    p.add_argument("--model", default="res15")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, seconds):
+    """Oracle (numpy fp32 im2col+BLAS restatement) on the host cores: bounded sample."""
+    from oracle import ref_numpy as orc
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count()
+    params = orc.make_params(cfg, 0)
+    rng = np.random.Generator(np.random.PCG64(1))
+    per = 4
+    x = rng.standard_normal((per, 101, 40)).astype(np.float32)
+    orc.forward(params, cfg, x[:1], acc=np.float32)  # warm-up
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.forward(params, cfg, x, acc=np.float32)
+        n += per
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "clips/s", "cores": int(cores), "kind": "port",
+            "sample": f"{n} clips of {cfg_name(cfg)} in {dt:.1f} s (oracle/ref_numpy.py fp32, batches of {per})"}
+
+
+def cfg_name(cfg):
+    return f"res{cfg['n_layers']}-{cfg['n_feature_maps']}maps" if "n_layers" in cfg else "cnn"
+
+
+def load_traffic():
+    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC pass (or None)."""
+    p = os.path.join(REPO, "profiles", "pmc_block_kernel.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from honk_amd import _native
+    from honk_amd import model as hm
+    from oracle import ref_numpy as orc
+
+    cfg = dict(hm.find_config(args.model))
+    torch.manual_seed(0)
+    model = hm.find_model(args.model)(cfg).eval().to(dev)
+    B = args.batch
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.randn(B, 101, 40, device=dev, generator=g)  # resident in HBM before timing
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            model(x)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        _native.timing_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = model(x)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier()
+        kms, nlaunch, kflop = _native.timing_read()
+        _native.timing_enable(False)
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # top-1 agreement of the GPU logits with the float64 oracle on a few clips
+    idx = [0, B // 3, B - 1]
+    xs = x[idx].cpu().numpy()
+    ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()},
+                      cfg, xs)
+    got = out[idx].cpu().numpy()
+    top1 = float(np.mean(np.argmax(ref, 1) == np.argmax(got, 1)))
+    maxerr = float(np.abs(ref - got).max())
+
+    total = world * B * args.steps
+    value = total / elapsed
+    flop_clip = orc.flops_per_clip(cfg)
+    avg_ms = kms / max(nlaunch, 1)
+    achieved = (kflop / max(nlaunch, 1)) / (avg_ms * 1e-3) / 1e12 if nlaunch else None
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "clips/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic N(0,1) [B,101,40] fp32 MFCC-shaped input resident in HBM; random-init weights",
+            "config": {"workload": f"{args.model} eval forward (SpeechResModel, 13 dilated 3x3 res layers, 45 maps,"
+                                   f" 12 labels)" if args.model == "res15" else f"{args.model} eval forward",
+                       "per_gpu_batch": B, "global_batch": world * B,
+                       "parallelism": f"batch-shard x{world} (no data-path collective)"},
+            "model_tflops": round(value * flop_clip / 1e12, 2),
+            "roofline": {"bound": "mfma", "kernel": "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)",
+                         "achieved": round(achieved, 2) if achieved else None,
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+                         "traffic": load_traffic(),
+                         "launches": nlaunch, "avg_launch_ms": round(avg_ms, 4),
+                         "flop_per_launch": kflop / max(nlaunch, 1)},
+            "parity": {"top1_agreement_vs_oracle": top1, "max_abs_logit_err_vs_oracle_f64": maxerr,
+                       "sample_clips": len(idx)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+"""ctypes binding of libhonk_hip.so (include/honk_hip.h).
+
+The shared library is the product's compute path for GPU tensors.  It is loaded
+lazily; if it is missing or fails to load, every native call raises
+``RuntimeError`` -- there is no silent fallback for device tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhonk_hip.so")
+
+c_f32p = ctypes.c_void_p
+
+
+class ResDesc(ctypes.Structure):
+    """honk_res_desc -- mirrors the SpeechResModel config keys (utils/model.py:85-92)."""
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n_labels", "n_maps", "n_layers", "use_dilation", "pool_h", "pool_w", "height", "width")]
+
+
+class CnnDesc(ctypes.Structure):
+    """honk_cnn_desc -- mirrors the SpeechModel config keys (utils/model.py:126-180)."""
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "height", "width", "n_labels",
+        "c1_out", "c1_kh", "c1_kw", "c1_sh", "c1_sw", "p1_h", "p1_w",
+        "has_conv2", "c2_out", "c2_kh", "c2_kw", "c2_sh", "c2_sw", "p2_h", "p2_w",
+        "has_lin", "dnn1", "dnn2", "dnn1_relu")]
+
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    "honk_res_packed_floats": (ctypes.c_size_t, [ctypes.POINTER(ResDesc)]),
+    "honk_res_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(ResDesc), ctypes.c_int64]),
+    "honk_res_pack": (ctypes.c_int, [ctypes.POINTER(ResDesc), ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32,
+                                     c_f32p, ctypes.c_void_p]),
+    "honk_res_forward": (ctypes.c_int, [ctypes.POINTER(ResDesc), c_f32p, c_f32p, c_f32p, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_cnn_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(CnnDesc), ctypes.c_int64]),
+    "honk_cnn_forward": (ctypes.c_int, [ctypes.POINTER(CnnDesc), ctypes.POINTER(ctypes.c_void_p), c_f32p, c_f32p,
+                                        ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_conv2d_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 10
+                        + [ctypes.c_void_p]),
+    "honk_maxpool2d_f32": (ctypes.c_int, [c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 5
+                           + [ctypes.c_void_p]),
+    "honk_linear_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, c_f32p, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
+    "honk_last_error": (ctypes.c_char_p, []),
+    "honk_version": (ctypes.c_char_p, []),
+    "honk_timing_enable": (ctypes.c_int, [ctypes.c_int32]),
+    "honk_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_double)]),
+}
+
+EXPORTS = tuple(_PROTOS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the ctypes library; raise RuntimeError if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"honk_amd: HIP extension not built ({path} missing); run `python -m honk_amd.build`")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:  # pragma: no cover - depends on ROCm install
+            raise RuntimeError(f"honk_amd: cannot load {path}: {e}") from e
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().honk_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+def version() -> str:
+    return load().honk_version().decode()
+
+
+def ptr(t) -> int:
+    return t.data_ptr() if t is not None else 0
+
+
+def ptr_array(tensors):
+    arr = (ctypes.c_void_p * len(tensors))()
+    for i, t in enumerate(tensors):
+        arr[i] = ptr(t) if t is not None else None
+    return arr
+
+
+def stream_handle(device) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def timing_enable(on: bool):
+    check(load().honk_timing_enable(1 if on else 0), "honk_timing_enable")
+
+
+def timing_read():
+    ms = ctypes.c_double()
+    n = ctypes.c_int64()
+    fl = ctypes.c_double()
+    check(load().honk_timing_read(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)), "honk_timing_read")
+    return ms.value, n.value, fl.value

@@ -1,0 +1,59 @@
+// Shared host/device helpers for libhonk_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/honk_hip.h"
+
+namespace honk {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// thread-local last error; set by fail(), read through honk_last_error()
+void set_error(const char* fmt, ...);
+const char* get_error();
+
+inline int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  set_error("%s", buf);
+  return code;
+}
+
+#define HONK_HIP_CHECK(expr)                                                           \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return ::honk::fail(HONK_ERR_HIP, "%s failed: %s (%s:%d)", #expr,                \
+                          hipGetErrorString(_e), __FILE__, __LINE__);                  \
+  } while (0)
+
+#define HONK_LAUNCH_CHECK(name)                                                        \
+  do {                                                                                 \
+    hipError_t _e = hipGetLastError();                                                 \
+    if (_e != hipSuccess)                                                              \
+      return ::honk::fail(HONK_ERR_HIP, "launch of %s failed: %s", name,               \
+                          hipGetErrorString(_e));                                      \
+  } while (0)
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// number of CUs of the current device (cached per device)
+int cu_count();
+
+// kernel timing window (honk_timing_*): wraps one launch with hipEvents
+struct TimedLaunch {
+  hipEvent_t start = nullptr, stop = nullptr;
+  bool on = false;
+  TimedLaunch(hipStream_t s, double flop);
+  void done(hipStream_t s);
+};
+
+}  // namespace honk

@@ -1,0 +1,655 @@
+// SpeechResModel forward (res8/15/26[-narrow]) for gfx950, fp32.
+//
+// Reference: /root/reference/utils/model.py:82-121.  The per-layer schedule
+// (model.py:104-121) is
+//     y = relu(conv_i(x)); i==0: y = pool(y), old = y
+//     i>0 even: x = y + old, old = x    else: x = y
+//     i>0: x = bn_i(x)                  (eval: (x-mean)/sqrt(var+1e-5))
+//     logits = Linear(mean_hw(x))
+//
+// HBM layout: activations are NHWC with the channel dim padded to CP = 16*NT
+// (CP = 48 for 45 maps, 32 for 19 maps); padded channels are kept at exactly 0.
+// Three activation buffers per batch chunk:
+//     R   pre-BN residual stream ("old_x"; written in place by even layers)
+//     X0/X1  BN-applied layer outputs = the next conv's input (ping-pong)
+// so every conv reads an already-normalised input (zero padding is then exactly
+// the reference's post-BN zero padding) and the epilogue fuses ReLU, residual
+// add, BN and both stores.
+//
+// Kernels
+//   conv0_kernel   1->C 3x3 pad 1 + ReLU + optional avg-pool, VALU (1.6 MMAC/clip)
+//   block_kernel   C->C 3x3 dilated conv as an implicit GEMM on fp32 MFMA
+//                  (v_mfma_f32_16x16x4_f32): M = pixels of a row band, N = CP
+//                  out-channels, K = 9 taps x CP in-channels.  Persistent grid,
+//                  one 64*4*NT-thread workgroup per CU; wave (nt, mg) owns
+//                  out-channel tile nt and MT 16-pixel m-tiles; its B operand
+//                  (the layer's weights for tile nt) is streamed from L2 one
+//                  row-offset (3 taps, 3*CP/4 VGPRs) per stage.  The A operand is staged per
+//                  (tile, dy) as a band of TH full rows shifted by (dy-1)*dil,
+//                  copied HBM/L2 -> LDS by buffer_load...lds (16 B per lane)
+//                  double-buffered against the MFMA work; the dx shift and the
+//                  column zero padding are folded into per-lane LDS addresses
+//                  (an out-of-range column reads a zero pixel kept in LDS); row
+//                  padding comes from the buffer bounds check (reads as 0).
+//   tail_kernel    spatial mean + Linear(C, n_labels) (model.py:119-121)
+#include "common.h"
+
+namespace honk {
+namespace res {
+
+constexpr int MW = 4;  // waves along M per workgroup
+
+template <int NT, int MT>
+struct Geo {
+  static constexpr int CP = 16 * NT;          // padded channels
+  static constexpr int Q = CP / 16;           // 16-channel k-quads per tap (= NT)
+  static constexpr int CH4 = CP / 4;          // 16-byte chunks per pixel
+  static constexpr int NWAVES = NT * MW;
+  static constexpr int NTHREADS = 64 * NWAVES;
+  static constexpr int MP = 16 * MT * MW;     // max pixels per tile
+  static constexpr int ZOFF = ((MP * CP + 255) / 256) * 256;  // zero pixel (floats)
+  static constexpr int BUF = ZOFF + CP;       // floats per LDS stage buffer
+};
+
+struct BlockArgs {
+  const float* in;        // [n][H][W][CP]  BN-applied input
+  const float* res;       // [n][H][W][CP]  residual (pre-BN) or nullptr
+  float* out_pre;         // pre-BN output (residual stream) or nullptr
+  float* out_bn;          // BN-applied output
+  const float* wfrag;     // [NT][9][Q][64][4] B fragments
+  const float* bn_scale;  // [CP]
+  const float* bn_shift;  // [CP]
+  int H, W, dil, TH, nbands, ntiles;
+};
+
+// A-operand staging: one (tile, dy) band of TH rows x W pixels x CP channels,
+// HBM/L2 -> LDS by buffer_load ... lds (16 B per lane, LDS image lane-linear).
+// Rows outside [0, H) get an out-of-range offset: the buffer bounds check
+// returns zeros, which is exactly the reference's zero padding.
+template <int NT, int MT>
+__device__ __forceinline__ void issue_stage(const BlockArgs& a, int tile, int dy, float* buf, int wave,
+                                            int lane) {
+  using G = Geo<NT, MT>;
+  const int b = tile / a.nbands;
+  const int h0 = (tile - b * a.nbands) * a.TH;
+  const int clip_floats = a.H * a.W * G::CP;
+  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.in + (size_t)b * clip_floats), (short)0, clip_floats * 4, 0x00020000);
+  const int total = a.TH * a.W * G::CH4;
+  const int npieces = (total + 63) >> 6;
+  const int rshift = (dy - 1) * a.dil;
+  for (int pc = wave; pc < npieces; pc += G::NWAVES) {
+    const int ci = (pc << 6) + lane;
+    const int pix = ci / G::CH4;
+    const int ch = ci - pix * G::CH4;
+    const int r = pix / a.W;
+    const int w = pix - r * a.W;
+    const int grow = h0 + r + rshift;
+    const bool ok = (ci < total) && (grow >= 0) && (grow < a.H);
+    const unsigned voff = ok ? (unsigned)(((grow * a.W + w) * G::CP + ch * 4) * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(buf + (pc << 8)),
+                                             16, voff, 0, 0, 0);
+  }
+}
+
+// One (dx, q) step of a stage: reads the A fragments of step K+1 while the
+// MFMAs of step K run.  Template recursion keeps every register index static.
+template <int NT, int MT, int K>
+__device__ __forceinline__ void stage_step(const char* base, const int (&aoff)[3][MT],
+                                           const f32x4 (&bcur)[3][NT], f32x4 (&acc)[MT],
+                                           f32x4 (&a0)[MT], f32x4 (&a1)[MT]) {
+  constexpr int NK = 3 * NT;
+  if constexpr (K < NK) {
+    constexpr int dx = K / NT, q = K % NT;
+    f32x4 (&cur)[MT] = (K & 1) ? a1 : a0;
+    f32x4 (&nxt)[MT] = (K & 1) ? a0 : a1;
+    if constexpr (K + 1 < NK) {
+      constexpr int dx1 = (K + 1) / NT, q1 = (K + 1) % NT;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) nxt[m] = *(const f32x4*)(base + aoff[dx1][m] + q1 * 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[m][j], bcur[dx][q][j], acc[m], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    stage_step<NT, MT, K + 1>(base, aoff, bcur, acc, a0, a1);
+  }
+}
+
+template <int NT, int MT>
+__device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff)[3][MT],
+                                              const f32x4 (&bcur)[3][NT], f32x4 (&acc)[MT]) {
+  const char* base = (const char*)cur;
+  f32x4 a0[MT], a1[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) a0[m] = *(const f32x4*)(base + aoff[0][m]);
+  stage_step<NT, MT, 0>(base, aoff, bcur, acc, a0, a1);
+}
+
+// B fragments of the 3 taps of row offset dy: frag[nt][tap][q][lane][4], read
+// through a buffer descriptor (lane offset in one VGPR, tap/q offset in SGPR).
+template <int NT>
+__device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t wr, int dy, int lane16, f32x4 (&b)[3][NT]) {
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+      b[dx][q] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, lane16, ((dy * 3 + dx) * NT + q) * 1024, 0));
+}
+
+template <int NT, int MT>
+__global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(BlockArgs a) {
+  using G = Geo<NT, MT>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * G::BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nt = wave % NT;
+  const int mg = wave / NT;
+  const int g = lane >> 4;
+  const int i16 = lane & 15;
+
+  for (int t = tid; t < G::CP; t += G::NTHREADS) {
+    smem[G::ZOFF + t] = 0.f;
+    smem[G::BUF + G::ZOFF + t] = 0.f;
+  }
+
+  // B operand: the layer's weights for out-channel tile nt, streamed from L2 one
+  // row offset (3 taps) per stage; the next stage's fragments are loaded right
+  // after this stage's MFMAs and land while the wave waits at the barrier
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.wfrag + (size_t)nt * 9 * G::Q * 64 * 4), (short)0, 9 * G::Q * 64 * 16, 0x00020000);
+  const int lane16 = lane * 16;
+  f32x4 bcur[3][NT];
+  load_b<NT>(wr, 0, lane16, bcur);
+
+  // A operand addresses (bytes within a stage buffer), one per (dx, m-tile)
+  const int TP = a.TH * a.W;
+  int aoff[3][MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int p = (mg * MT + m) * 16 + i16;
+    const int r = p / a.W;
+    const int w = p - r * a.W;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int sh = (dx - 1) * a.dil;
+      const int col = w + sh;
+      const bool ok = (p < TP) && (col >= 0) && (col < a.W);
+      aoff[dx][m] = ok ? ((p + sh) * G::CP + g * 4) * 4 : (G::ZOFF + g * 4) * 4;
+    }
+  }
+
+  const int cout = nt * 16 + i16;
+  const float bsc = a.bn_scale[cout];
+  const float bsh = a.bn_shift[cout];
+
+  // XCD-aware tile order: blocks sharing an XCD (bid % 8) walk adjacent tiles
+  const int GR = gridDim.x;
+  const int bid = blockIdx.x;
+  const int lb = ((GR & 7) == 0) ? (bid & 7) * (GR >> 3) + (bid >> 3) : bid;
+  int tile = lb;
+  if (tile >= a.ntiles) return;
+
+  int s = 0;
+  issue_stage<NT, MT>(a, tile, 0, smem, wave, lane);
+  while (true) {
+    f32x4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define HONK_STAGE(DY)                                                                  \
+  {                                                                                     \
+    float* cur = smem + (s & 1) * G::BUF;                                               \
+    float* nxt = smem + ((s + 1) & 1) * G::BUF;                                         \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                    \
+    __syncthreads();                                                                    \
+    if (DY < 2)                                                                         \
+      issue_stage<NT, MT>(a, tile, DY + 1, nxt, wave, lane);                            \
+    else if (tile + GR < a.ntiles)                                                      \
+      issue_stage<NT, MT>(a, tile + GR, 0, nxt, wave, lane);                            \
+    compute_stage<NT, MT>(cur, aoff, bcur, acc);                                        \
+    load_b<NT>(wr, (DY + 1) % 3, lane16, bcur); /* lands while waiting at the barrier */ \
+    ++s;                                                                                \
+  }
+    HONK_STAGE(0)
+    HONK_STAGE(1)
+    HONK_STAGE(2)
+#undef HONK_STAGE
+
+    // epilogue: ReLU (+ residual) -> pre-BN store (even layers) and BN store.
+    // C/D layout of 16x16x4: lane holds rows g*4+r (pixels) of column i16 (cout).
+    {
+      const int b = tile / a.nbands;
+      const int h0 = (tile - b * a.nbands) * a.TH;
+      const size_t tbase = ((size_t)b * a.H + h0) * a.W * G::CP;  // wave-uniform
+      int ebase = (mg * MT * 16 + g * 4) * G::CP + cout;
+      int lim = min(a.TH, a.H - h0) * a.W - (mg * MT * 16 + g * 4);
+      asm volatile("" : "+v"(ebase), "+v"(lim));  // keep these from being hoisted/expanded
+      const float* res_t = a.res ? a.res + tbase : nullptr;
+      float* pre_t = a.out_pre ? a.out_pre + tbase : nullptr;
+      float* bn_t = a.out_bn + tbase;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (m * 16 + r < lim) {
+            const int idx = ebase + (m * 16 + r) * G::CP;
+            float v = fmaxf(acc[m][r], 0.f);
+            if (res_t) v += res_t[idx];
+            if (pre_t) pre_t[idx] = v;
+            bn_t[idx] = fmaf(v, bsc, bsh);
+          }
+        }
+      }
+    }
+    tile += GR;
+    if (tile >= a.ntiles) break;
+  }
+}
+
+// --------------------------------------------------------------------------- //
+// conv0: 1 -> C, 3x3, pad 1, ReLU, optional avg-pool (PH x PW); NHWC(CP) out
+// --------------------------------------------------------------------------- //
+template <int PH, int PW>
+__global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                    const float* __restrict__ w0, int n, int Hin,
+                                                    int Win, int H, int W, int C, int CP) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)n * H * W;
+  if (gid >= total) return;
+  const int ow = (int)(gid % W);
+  const int64_t t = gid / W;
+  const int oh = (int)(t % H);
+  const int b = (int)(t / H);
+  const float* xb = x + (int64_t)b * Hin * Win;
+  // input window rows [oh*PH-1, oh*PH+PH], cols [ow*PW-1, ow*PW+PW]
+  float win[PH + 2][PW + 2];
+#pragma unroll
+  for (int r = 0; r < PH + 2; ++r) {
+    const int ir = oh * PH - 1 + r;
+#pragma unroll
+    for (int c = 0; c < PW + 2; ++c) {
+      const int ic = ow * PW - 1 + c;
+      win[r][c] = (ir >= 0 && ir < Hin && ic >= 0 && ic < Win) ? xb[(int64_t)ir * Win + ic] : 0.f;
+    }
+  }
+  float* o = out + gid * CP;
+  const float inv = 1.0f / (float)(PH * PW);
+  for (int c4 = 0; c4 < CP; c4 += 4) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c4 + u;
+      float s = 0.f;
+      if (c < C) {
+        const float* wc = w0 + c * 9;
+        float wr[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) wr[k] = wc[k];
+#pragma unroll
+        for (int a = 0; a < PH; ++a)
+#pragma unroll
+          for (int bb = 0; bb < PW; ++bb) {
+            float acc = 0.f;
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+              for (int kx = 0; kx < 3; ++kx) acc = fmaf(win[a + ky][bb + kx], wr[ky * 3 + kx], acc);
+            s += fmaxf(acc, 0.f);
+          }
+        if (PH * PW > 1) s *= inv;
+      }
+      v[u] = s;
+    }
+    *(f32x4*)(o + c4) = f32x4{v[0], v[1], v[2], v[3]};
+  }
+}
+
+// generic pool shape (any PH, PW): same math, input read through L1
+__global__ __launch_bounds__(256) void conv0_generic_kernel(const float* __restrict__ x,
+                                                            float* __restrict__ out,
+                                                            const float* __restrict__ w0, int n,
+                                                            int Hin, int Win, int H, int W, int C,
+                                                            int CP, int PH, int PW) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)n * H * W;
+  if (gid >= total) return;
+  const int ow = (int)(gid % W);
+  const int64_t t = gid / W;
+  const int oh = (int)(t % H);
+  const int b = (int)(t / H);
+  const float* xb = x + (int64_t)b * Hin * Win;
+  float* o = out + gid * CP;
+  const float inv = 1.0f / (float)(PH * PW);
+  for (int c = 0; c < CP; ++c) {
+    float s = 0.f;
+    if (c < C) {
+      for (int a = 0; a < PH; ++a)
+        for (int bb = 0; bb < PW; ++bb) {
+          float acc = 0.f;
+          for (int ky = 0; ky < 3; ++ky)
+            for (int kx = 0; kx < 3; ++kx) {
+              const int ir = oh * PH + a + ky - 1, ic = ow * PW + bb + kx - 1;
+              const float xv = (ir >= 0 && ir < Hin && ic >= 0 && ic < Win) ? xb[(int64_t)ir * Win + ic] : 0.f;
+              acc = fmaf(xv, w0[c * 9 + ky * 3 + kx], acc);
+            }
+          s += fmaxf(acc, 0.f);
+        }
+      if (PH * PW > 1) s *= inv;
+    }
+    o[c] = s;
+  }
+}
+
+// --------------------------------------------------------------------------- //
+// tail: logits[b] = Wout . mean_hw(x[b]) + bout      (x already BN-applied)
+// --------------------------------------------------------------------------- //
+__global__ __launch_bounds__(256) void tail_kernel(const float* __restrict__ x, const float* __restrict__ wout,
+                                                   const float* __restrict__ bout, float* __restrict__ logits,
+                                                   int HW, int C, int CP, int NL) {
+  __shared__ float part[256];
+  __shared__ float mean[64];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int groups = blockDim.x / CP;  // pixel groups
+  const int c = tid % CP;
+  const int pg = tid / CP;
+  float s = 0.f;
+  if (pg < groups) {
+    const float* xb = x + (int64_t)b * HW * CP + c;
+    for (int p = pg; p < HW; p += groups) s += xb[(int64_t)p * CP];
+  }
+  part[tid] = s;
+  __syncthreads();
+  if (tid < CP) {
+    float t = 0.f;
+    for (int q = 0; q < groups; ++q) t += part[q * CP + tid];
+    mean[tid] = t / (float)HW;
+  }
+  __syncthreads();
+  for (int nlab = tid; nlab < NL; nlab += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < C; ++k) acc = fmaf(wout[nlab * C + k], mean[k], acc);
+    logits[(int64_t)b * NL + nlab] = acc + bout[nlab];
+  }
+}
+
+// --------------------------------------------------------------------------- //
+// weight packing
+// --------------------------------------------------------------------------- //
+__global__ void pack_conv0_kernel(const float* __restrict__ w, float* __restrict__ out, int C, int CP) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= CP * 9) return;
+  const int c = i / 9;
+  out[i] = (c < C) ? w[i] : 0.f;
+}
+
+// frag[nt][tap][q][lane][j] = W[co = nt*16 + (lane&15)][ci = 16q + 4(lane>>4) + j][tap]
+__global__ void pack_block_kernel(const float* __restrict__ w, float* __restrict__ frag, int C, int NT) {
+  const int CP = 16 * NT;
+  const int Q = CP / 16;
+  const int total = NT * 9 * Q * 4 * 64;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int r = i;
+  const int j = r & 3; r >>= 2;
+  const int lane = r & 63; r >>= 6;
+  const int q = r % Q; r /= Q;
+  const int tap = r % 9; r /= 9;
+  const int nt = r;
+  const int co = nt * 16 + (lane & 15);
+  const int ci = 16 * q + 4 * (lane >> 4) + j;
+  frag[i] = (co < C && ci < C) ? w[((size_t)co * C + ci) * 9 + tap] : 0.f;
+}
+
+__global__ void pack_bn_kernel(const float* __restrict__ mean, const float* __restrict__ var,
+                               float* __restrict__ scale, float* __restrict__ shift, int C, int CP) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= CP) return;
+  if (c < C) {
+    const float inv = 1.0f / sqrtf(var[c] + 1e-5f);
+    scale[c] = inv;
+    shift[c] = -mean[c] * inv;
+  } else {
+    scale[c] = 1.f;
+    shift[c] = 0.f;
+  }
+}
+
+__global__ void copy_kernel(const float* __restrict__ src, float* __restrict__ dst, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src ? src[i] : 0.f;
+}
+
+// --------------------------------------------------------------------------- //
+// host side
+// --------------------------------------------------------------------------- //
+struct Layout {
+  int C, CP, NT, L, NL;
+  int Hin, Win, H, W, ph, pw;
+  size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, total;
+};
+
+static size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
+
+static int make_layout(const honk_res_desc* d, Layout* L) {
+  if (!d) return fail(HONK_ERR_ARG, "null descriptor");
+  if (d->n_maps < 1 || d->n_layers < 0 || d->n_labels < 1 || d->height < 1 || d->width < 1)
+    return fail(HONK_ERR_ARG, "bad res descriptor (n_maps=%d n_layers=%d n_labels=%d h=%d w=%d)",
+                d->n_maps, d->n_layers, d->n_labels, d->height, d->width);
+  if (d->n_maps > 48)
+    return fail(HONK_ERR_UNSUPPORTED, "n_feature_maps=%d > 48 is not supported by the gfx950 kernels",
+                d->n_maps);
+  L->C = d->n_maps;
+  L->NT = (d->n_maps + 15) / 16;
+  L->CP = 16 * L->NT;
+  L->L = d->n_layers;
+  L->NL = d->n_labels;
+  L->Hin = d->height;
+  L->Win = d->width;
+  L->ph = d->pool_h > 0 ? d->pool_h : 1;
+  L->pw = d->pool_w > 0 ? d->pool_w : 1;
+  L->H = L->Hin / L->ph;
+  L->W = L->Win / L->pw;
+  if (L->H < 1 || L->W < 1) return fail(HONK_ERR_ARG, "pool larger than input");
+  L->off_conv0 = 0;
+  L->off_layers = round64((size_t)L->CP * 9);
+  L->layer_floats = (size_t)9 * L->CP * L->CP;
+  L->off_bn = L->off_layers + L->layer_floats * L->L;
+  L->off_wout = L->off_bn + round64((size_t)2 * L->CP * L->L);
+  L->off_bout = L->off_wout + round64((size_t)L->NL * L->C);
+  L->off_zeros = L->off_bout + round64((size_t)L->NL);
+  L->total = L->off_zeros + 64;
+  return HONK_OK;
+}
+
+static int64_t chunk_clips(const Layout& L, int64_t batch) {
+  const size_t per_clip = (size_t)L.H * L.W * L.CP * sizeof(float);
+  int64_t ch = (int64_t)((size_t)3 << 30) / (int64_t)per_clip;  // ~3 GiB per activation buffer
+  if (const char* e = getenv("HONK_RES_CHUNK")) ch = atoll(e);
+  if (ch < 1) ch = 1;
+  return batch < ch ? batch : ch;
+}
+
+struct Plan {
+  int NT, MT, TH, nbands;
+};
+
+// choose MT (m-tiles per wave) and TH (rows per band) to minimise padded work
+static Plan plan_block(const Layout& L) {
+  Plan best{L.NT, 4, 1, L.H};
+  double best_cost = 1e30;
+  const int mts[3] = {4, 5, 6};
+  for (int mi = 0; mi < 3; ++mi) {
+    const int MT = mts[mi];
+    const int MP = 16 * MT * MW;
+    const int thmax = MP / L.W;
+    if (thmax < 1) continue;
+    const int nb = (L.H + thmax - 1) / thmax;
+    const int th = (L.H + nb - 1) / nb;
+    // cost ~ padded pixels per clip (all m-tiles are computed)
+    const double cost = (double)nb * MP;
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = Plan{L.NT, MT, th, nb};
+    }
+  }
+  return best;
+}
+
+template <int NT, int MT>
+static int launch_block(const BlockArgs& a, hipStream_t st) {
+  using G = Geo<NT, MT>;
+  int grid = cu_count();
+  if (grid > a.ntiles) grid = a.ntiles;
+  hipLaunchKernelGGL((block_kernel<NT, MT>), dim3(grid), dim3(G::NTHREADS), 0, st, a);
+  HONK_LAUNCH_CHECK("res block_kernel");
+  return HONK_OK;
+}
+
+static int dispatch_block(const Plan& p, const BlockArgs& a, hipStream_t st) {
+#define HONK_CASE(nt, mt) \
+  if (p.NT == nt && p.MT == mt) return launch_block<nt, mt>(a, st);
+  HONK_CASE(1, 4) HONK_CASE(1, 5) HONK_CASE(1, 6)
+  HONK_CASE(2, 4) HONK_CASE(2, 5) HONK_CASE(2, 6)
+  HONK_CASE(3, 4) HONK_CASE(3, 5) HONK_CASE(3, 6)
+#undef HONK_CASE
+  return fail(HONK_ERR_UNSUPPORTED, "no block kernel for NT=%d MT=%d", p.NT, p.MT);
+}
+
+static int launch_conv0(const Layout& L, const float* x, float* out, const float* w0, int64_t n,
+                        hipStream_t st) {
+  const int64_t total = n * L.H * L.W;
+  const int blocks = (int)cdiv(total, 256);
+#define HONK_C0(PH, PW)                                                                        \
+  if (L.ph == PH && L.pw == PW) {                                                              \
+    hipLaunchKernelGGL((conv0_kernel<PH, PW>), dim3(blocks), dim3(256), 0, st, x, out, w0,     \
+                       (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                             \
+    HONK_LAUNCH_CHECK("res conv0_kernel");                                                     \
+    return HONK_OK;                                                                            \
+  }
+  HONK_C0(1, 1) HONK_C0(2, 2) HONK_C0(4, 3)
+#undef HONK_C0
+  hipLaunchKernelGGL(conv0_generic_kernel, dim3(blocks), dim3(256), 0, st, x, out, w0, (int)n, L.Hin,
+                     L.Win, L.H, L.W, L.C, L.CP, L.ph, L.pw);
+  HONK_LAUNCH_CHECK("res conv0_generic_kernel");
+  return HONK_OK;
+}
+
+}  // namespace res
+}  // namespace honk
+
+using namespace honk;
+using namespace honk::res;
+
+extern "C" {
+
+size_t honk_res_packed_floats(const honk_res_desc* d) {
+  Layout L;
+  if (make_layout(d, &L) != HONK_OK) return 0;
+  return L.total;
+}
+
+size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
+  Layout L;
+  if (make_layout(d, &L) != HONK_OK || batch < 1) return 0;
+  const int64_t ch = chunk_clips(L, batch);
+  return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float);
+}
+
+int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tensors, float* packed,
+                  void* stream) {
+  Layout L;
+  int rc = make_layout(d, &L);
+  if (rc) return rc;
+  if (!t || !packed) return fail(HONK_ERR_ARG, "null tensors/packed");
+  if (n_tensors != 3 * L.L + 3)
+    return fail(HONK_ERR_ARG, "honk_res_pack expects %d tensors, got %d", 3 * L.L + 3, n_tensors);
+  for (int i = 0; i < n_tensors; ++i)
+    if (!t[i]) return fail(HONK_ERR_ARG, "tensor %d is null", i);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(pack_conv0_kernel, dim3(cdiv(L.CP * 9, 256)), dim3(256), 0, st, t[0],
+                     packed + L.off_conv0, L.C, L.CP);
+  HONK_LAUNCH_CHECK("pack_conv0");
+  const int nfrag = (int)L.layer_floats;
+  for (int i = 0; i < L.L; ++i) {
+    hipLaunchKernelGGL(pack_block_kernel, dim3(cdiv(nfrag, 256)), dim3(256), 0, st, t[1 + i],
+                       packed + L.off_layers + (size_t)i * L.layer_floats, L.C, L.NT);
+    HONK_LAUNCH_CHECK("pack_block");
+    float* sc = packed + L.off_bn + (size_t)2 * L.CP * i;
+    hipLaunchKernelGGL(pack_bn_kernel, dim3(1), dim3(64), 0, st, t[1 + L.L + 2 * i],
+                       t[1 + L.L + 2 * i + 1], sc, sc + L.CP, L.C, L.CP);
+    HONK_LAUNCH_CHECK("pack_bn");
+  }
+  const int nw = L.NL * L.C;
+  hipLaunchKernelGGL(copy_kernel, dim3(cdiv(nw, 256)), dim3(256), 0, st, t[1 + 3 * L.L],
+                     packed + L.off_wout, nw);
+  hipLaunchKernelGGL(copy_kernel, dim3(cdiv(L.NL, 256)), dim3(256), 0, st, t[2 + 3 * L.L],
+                     packed + L.off_bout, L.NL);
+  hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(64), 0, st, (const float*)nullptr,
+                     packed + L.off_zeros, 64);
+  HONK_LAUNCH_CHECK("pack_copy");
+  return HONK_OK;
+}
+
+int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x, float* logits,
+                     int64_t batch, void* workspace, size_t ws_bytes, void* stream) {
+  Layout L;
+  int rc = make_layout(d, &L);
+  if (rc) return rc;
+  if (batch < 0) return fail(HONK_ERR_ARG, "negative batch");
+  if (batch == 0) return HONK_OK;
+  if (!packed || !x || !logits || !workspace) return fail(HONK_ERR_ARG, "null pointer argument");
+  const size_t need = honk_res_workspace_bytes(d, batch);
+  if (ws_bytes < need)
+    return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t chunk = chunk_clips(L, batch);
+  const size_t act = (size_t)chunk * L.H * L.W * L.CP;
+  float* R = (float*)workspace;
+  float* X[2] = {R + act, R + 2 * act};
+  const Plan p = plan_block(L);
+  const double layer_flop_per_clip = 2.0 * L.H * L.W * L.C * L.C * 9;
+
+  for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
+    const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
+    if ((int64_t)n * p.nbands > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
+    rc = launch_conv0(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+    if (rc) return rc;
+    for (int i = 1; i <= L.L; ++i) {
+      BlockArgs a;
+      a.in = (i == 1) ? R : X[i & 1];
+      const bool even = (i % 2) == 0;
+      a.res = even ? R : nullptr;
+      a.out_pre = even ? R : nullptr;
+      a.out_bn = X[(i + 1) & 1];
+      a.wfrag = packed + L.off_layers + (size_t)(i - 1) * L.layer_floats;
+      a.bn_scale = packed + L.off_bn + (size_t)2 * L.CP * (i - 1);
+      a.bn_shift = a.bn_scale + L.CP;
+      a.H = L.H;
+      a.W = L.W;
+      a.dil = d->use_dilation ? (1 << ((i - 1) / 3)) : 1;
+      a.TH = p.TH;
+      a.nbands = p.nbands;
+      a.ntiles = (int)(n * p.nbands);
+      TimedLaunch tl(st, layer_flop_per_clip * (double)n);
+      rc = dispatch_block(p, a, st);
+      tl.done(st);
+      if (rc) return rc;
+    }
+    const float* last = (L.L == 0) ? R : X[(L.L + 1) & 1];
+    hipLaunchKernelGGL(tail_kernel, dim3((unsigned)n), dim3(L.CP * (256 / L.CP)), 0, st, last,
+                       packed + L.off_wout, packed + L.off_bout, logits + c0 * L.NL, L.H * L.W, L.C,
+                       L.CP, L.NL);
+    HONK_LAUNCH_CHECK("res tail_kernel");
+  }
+  return HONK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,406 @@
+"""Drop-in model registry and modules: the call surface of /root/reference/utils/model.py.
+
+Same names, same config dicts, same constructor RNG consumption, same
+state_dict keys/shapes/dtypes as the reference, so ``utils/train.py`` and
+``service.py``-style callers work unchanged:
+
+* ``ConfigType``, ``find_model``, ``find_config``, ``_configs``   (model.py:33-62, 381-414)
+* ``truncated_normal``                                             (model.py:64-70)
+* ``SerializableModule.save/load``                                 (model.py:72-80)
+* ``SpeechResModel``                                               (model.py:82-121)
+* ``SpeechModel``                                                  (model.py:123-205)
+
+Forward dispatch:
+
+* eval mode on a ROCm (``cuda``) tensor -> the hand-written gfx950 kernels in
+  ``libhonk_hip.so`` (``honk_res_forward`` / ``honk_cnn_forward``).  If the
+  extension is missing this raises; there is no silent fallback.
+* CPU tensors, or training mode (autograd) -> the same PyTorch module ops the
+  reference runs (the reference is pure PyTorch; this keeps ``--no_cuda``
+  evaluation and ``train()`` working).  Native training kernels are future work
+  (DESIGN.md).
+"""
+from __future__ import annotations
+
+from enum import Enum
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native
+
+
+class ConfigType(Enum):
+    CNN_TRAD_POOL2 = "cnn-trad-pool2"  # default full model (TF variant)
+    CNN_ONE_STRIDE1 = "cnn-one-stride1"  # default compact model (TF variant)
+    CNN_ONE_FPOOL3 = "cnn-one-fpool3"
+    CNN_ONE_FSTRIDE4 = "cnn-one-fstride4"
+    CNN_ONE_FSTRIDE8 = "cnn-one-fstride8"
+    CNN_TPOOL2 = "cnn-tpool2"
+    CNN_TPOOL3 = "cnn-tpool3"
+    CNN_TSTRIDE2 = "cnn-tstride2"
+    CNN_TSTRIDE4 = "cnn-tstride4"
+    CNN_TSTRIDE8 = "cnn-tstride8"
+    RES15 = "res15"
+    RES26 = "res26"
+    RES8 = "res8"
+    RES15_NARROW = "res15-narrow"
+    RES8_NARROW = "res8-narrow"
+    RES26_NARROW = "res26-narrow"
+
+
+def find_model(conf):
+    """model.py:51-57 -- ``res*`` -> SpeechResModel, everything else -> SpeechModel."""
+    if isinstance(conf, ConfigType):
+        conf = conf.value
+    if conf.startswith("res"):
+        return SpeechResModel
+    return SpeechModel
+
+
+def find_config(conf):
+    """model.py:59-62 -- returns the SHARED dict (callers such as service.py:82 mutate it)."""
+    if isinstance(conf, ConfigType):
+        conf = conf.value
+    return _configs[conf]
+
+
+def truncated_normal(tensor, std_dev=0.01):
+    """model.py:64-70 -- resample |x| > 2 std until none remain (same RNG call sequence)."""
+    tensor.zero_()
+    tensor.normal_(std=std_dev)
+    while torch.sum(torch.abs(tensor) > 2 * std_dev) > 0:
+        t = tensor[torch.abs(tensor) > 2 * std_dev]
+        t.zero_()
+        tensor[torch.abs(tensor) > 2 * std_dev] = torch.normal(t, std=std_dev)
+
+
+class SerializableModule(nn.Module):
+    """model.py:72-80."""
+
+    def __init__(self):
+        super().__init__()
+
+    def save(self, filename):
+        torch.save(self.state_dict(), filename)
+
+    def load(self, filename):
+        # weights_only load: a state_dict holds tensors only
+        self.load_state_dict(torch.load(filename, map_location=lambda storage, loc: storage, weights_only=True))
+
+
+def _native_ready(x, module):
+    return x.is_cuda and not module.training
+
+
+def _state_key(tensors, device):
+    return (str(device),) + tuple((t.data_ptr(), t._version) for t in tensors)
+
+
+class SpeechResModel(SerializableModule):
+    """Deep residual KWS net (res8/15/26[-narrow]); model.py:82-121."""
+
+    def __init__(self, config):
+        super().__init__()
+        n_labels = config["n_labels"]
+        n_maps = config["n_feature_maps"]
+        self.conv0 = nn.Conv2d(1, n_maps, (3, 3), padding=(1, 1), bias=False)
+        if "res_pool" in config:
+            self.pool = nn.AvgPool2d(config["res_pool"])
+
+        self.n_layers = n_layers = config["n_layers"]
+        dilation = config["use_dilation"]
+        if dilation:
+            self.convs = [nn.Conv2d(n_maps, n_maps, (3, 3), padding=int(2 ** (i // 3)), dilation=int(2 ** (i // 3)),
+                                    bias=False) for i in range(n_layers)]
+        else:
+            self.convs = [nn.Conv2d(n_maps, n_maps, (3, 3), padding=1, dilation=1, bias=False)
+                          for _ in range(n_layers)]
+        for i, conv in enumerate(self.convs):
+            self.add_module("bn{}".format(i + 1), nn.BatchNorm2d(n_maps, affine=False))
+            self.add_module("conv{}".format(i + 1), conv)
+        self.output = nn.Linear(n_maps, n_labels)
+
+        pool = config.get("res_pool")
+        self._honk_desc = dict(n_labels=int(n_labels), n_maps=int(n_maps), n_layers=int(n_layers),
+                               use_dilation=int(bool(dilation)),
+                               pool_h=int(pool[0]) if pool is not None else 0,
+                               pool_w=int(pool[1]) if pool is not None else 0)
+        self._honk_packed = None
+        self._honk_key = None
+
+    # -- reference forward (CPU tensors / training mode): model.py:104-121 --
+    def _torch_forward(self, x):
+        x = x.unsqueeze(1)
+        for i in range(self.n_layers + 1):
+            y = F.relu(getattr(self, "conv{}".format(i))(x))
+            if i == 0:
+                if hasattr(self, "pool"):
+                    y = self.pool(y)
+                old_x = y
+            if i > 0 and i % 2 == 0:
+                x = y + old_x
+                old_x = x
+            else:
+                x = y
+            if i > 0:
+                x = getattr(self, "bn{}".format(i))(x)
+        x = x.view(x.size(0), x.size(1), -1)  # shape: (batch, feats, o3)
+        x = torch.mean(x, 2)
+        return self.output(x)
+
+    # -- native gfx950 path ------------------------------------------------------
+    def _pack_tensors(self):
+        L = self.n_layers
+        ts = [self.conv0.weight]
+        ts += [getattr(self, f"conv{i}").weight for i in range(1, L + 1)]
+        for i in range(1, L + 1):
+            bn = getattr(self, f"bn{i}")
+            ts += [bn.running_mean, bn.running_var]
+        ts += [self.output.weight, self.output.bias]
+        return ts
+
+    def _desc(self, height, width):
+        d = _native.ResDesc(height=height, width=width, **self._honk_desc)
+        return d
+
+    def _packed(self, x):
+        lib = _native.load()
+        ts = self._pack_tensors()
+        key = _state_key(ts, x.device)
+        if self._honk_packed is not None and self._honk_key == key:
+            return self._honk_packed
+        for t in ts:
+            if t.device != x.device or t.dtype != torch.float32:
+                raise RuntimeError(f"honk_amd: parameters must be float32 on {x.device} (got {t.dtype} on {t.device})")
+        ts = [t.detach().contiguous() for t in ts]
+        desc = self._desc(x.shape[1], x.shape[2])
+        n = lib.honk_res_packed_floats(desc)
+        if n == 0:
+            _native.check(-1, "honk_res_packed_floats")
+        packed = torch.empty(n, dtype=torch.float32, device=x.device)
+        arr = _native.ptr_array(ts)
+        _native.check(lib.honk_res_pack(desc, arr, len(ts), packed.data_ptr(), _native.stream_handle(x.device)),
+                      "honk_res_pack")
+        self._honk_packed, self._honk_key = packed, key
+        self._honk_keep = ts  # keep contiguous copies alive until the pack kernels ran
+        return packed
+
+    def _native_forward(self, x):
+        if x.dim() != 3:
+            raise RuntimeError(f"SpeechResModel expects [B, H, W] input, got {tuple(x.shape)}")
+        if x.dtype != torch.float32:
+            raise RuntimeError(f"expected float32 input, got {x.dtype}")
+        x = x.contiguous()
+        lib = _native.load()
+        with torch.cuda.device(x.device):
+            packed = self._packed(x)
+            desc = self._desc(x.shape[1], x.shape[2])
+            B = x.shape[0]
+            out = torch.empty(B, self._honk_desc["n_labels"], dtype=torch.float32, device=x.device)
+            if B == 0:
+                return out
+            ws_bytes = lib.honk_res_workspace_bytes(desc, B)
+            if ws_bytes == 0:
+                _native.check(-1, "honk_res_workspace_bytes")
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+            _native.check(lib.honk_res_forward(desc, packed.data_ptr(), x.data_ptr(), out.data_ptr(), B,
+                                               ws.data_ptr(), ws_bytes, _native.stream_handle(x.device)),
+                          "honk_res_forward")
+        return out
+
+    def forward(self, x):
+        if _native_ready(x, self):
+            return self._native_forward(x)
+        return self._torch_forward(x)
+
+
+class SpeechModel(SerializableModule):
+    """TF-style KWS CNNs (cnn-trad-pool2, cnn-one-*, ...); model.py:123-205."""
+
+    def __init__(self, config):
+        super().__init__()
+        n_labels = config["n_labels"]
+        n_featmaps1 = config["n_feature_maps1"]
+
+        conv1_size = config["conv1_size"]  # (time, frequency)
+        conv1_pool = config["conv1_pool"]
+        conv1_stride = tuple(config["conv1_stride"])
+        dropout_prob = config["dropout_prob"]
+        width = config["width"]
+        height = config["height"]
+        self.conv1 = nn.Conv2d(1, n_featmaps1, conv1_size, stride=conv1_stride)
+        tf_variant = config.get("tf_variant")
+        self.tf_variant = tf_variant
+        if tf_variant:
+            truncated_normal(self.conv1.weight.data)
+            self.conv1.bias.data.zero_()
+        self.pool1 = nn.MaxPool2d(conv1_pool)
+
+        with torch.no_grad():  # shape probe, model.py:143-160 (consumes no RNG)
+            x = torch.zeros(1, 1, height, width)
+            x = self.pool1(self.conv1(x))
+            conv_net_size = x.view(1, -1).size(1)
+            last_size = conv_net_size
+
+            desc = dict(height=int(height), width=int(width), n_labels=int(n_labels),
+                        c1_out=int(n_featmaps1), c1_kh=int(conv1_size[0]), c1_kw=int(conv1_size[1]),
+                        c1_sh=int(conv1_stride[0]), c1_sw=int(conv1_stride[1]),
+                        p1_h=int(_pair(conv1_pool)[0]), p1_w=int(_pair(conv1_pool)[1]),
+                        has_conv2=0, c2_out=0, c2_kh=0, c2_kw=0, c2_sh=1, c2_sw=1, p2_h=1, p2_w=1,
+                        has_lin=0, dnn1=0, dnn2=0, dnn1_relu=int(not tf_variant))
+            if "conv2_size" in config:
+                conv2_size = config["conv2_size"]
+                conv2_pool = config["conv2_pool"]
+                conv2_stride = tuple(config["conv2_stride"])
+                n_featmaps2 = config["n_feature_maps2"]
+                self.conv2 = nn.Conv2d(n_featmaps1, n_featmaps2, conv2_size, stride=conv2_stride)
+                if tf_variant:
+                    truncated_normal(self.conv2.weight.data)
+                    self.conv2.bias.data.zero_()
+                self.pool2 = nn.MaxPool2d(conv2_pool)
+                x = self.pool2(self.conv2(x))
+                conv_net_size = x.view(1, -1).size(1)
+                last_size = conv_net_size
+                desc.update(has_conv2=1, c2_out=int(n_featmaps2), c2_kh=int(conv2_size[0]),
+                            c2_kw=int(conv2_size[1]), c2_sh=int(conv2_stride[0]), c2_sw=int(conv2_stride[1]),
+                            p2_h=int(_pair(conv2_pool)[0]), p2_w=int(_pair(conv2_pool)[1]))
+        if not tf_variant:
+            self.lin = nn.Linear(conv_net_size, 32)
+            desc["has_lin"] = 1
+
+        if "dnn1_size" in config:
+            dnn1_size = config["dnn1_size"]
+            last_size = dnn1_size
+            if tf_variant:
+                self.dnn1 = nn.Linear(conv_net_size, dnn1_size)
+                truncated_normal(self.dnn1.weight.data)
+                self.dnn1.bias.data.zero_()
+            else:
+                self.dnn1 = nn.Linear(32, dnn1_size)
+            desc["dnn1"] = int(dnn1_size)
+            if "dnn2_size" in config:
+                dnn2_size = config["dnn2_size"]
+                last_size = dnn2_size
+                self.dnn2 = nn.Linear(dnn1_size, dnn2_size)
+                if tf_variant:
+                    truncated_normal(self.dnn2.weight.data)
+                    self.dnn2.bias.data.zero_()
+                desc["dnn2"] = int(dnn2_size)
+        self.output = nn.Linear(last_size, n_labels)
+        if tf_variant:
+            truncated_normal(self.output.weight.data)
+            self.output.bias.data.zero_()
+        self.dropout = nn.Dropout(dropout_prob)
+        self._honk_desc = desc
+
+    # -- reference forward (CPU tensors / training mode): model.py:186-205 --
+    def _torch_forward(self, x):
+        x = F.relu(self.conv1(x.unsqueeze(1)))  # shape: (batch, channels, i1, o1)
+        x = self.dropout(x)
+        x = self.pool1(x)
+        if hasattr(self, "conv2"):
+            x = F.relu(self.conv2(x))  # shape: (batch, o1, i2, o2)
+            x = self.dropout(x)
+            x = self.pool2(x)
+        x = x.view(x.size(0), -1)  # shape: (batch, o3)
+        if hasattr(self, "lin"):
+            x = self.lin(x)
+        if hasattr(self, "dnn1"):
+            x = self.dnn1(x)
+            if not self.tf_variant:
+                x = F.relu(x)
+            x = self.dropout(x)
+        if hasattr(self, "dnn2"):
+            x = self.dnn2(x)
+            x = self.dropout(x)
+        return self.output(x)
+
+    def _native_tensors(self):
+        def wb(name):
+            m = getattr(self, name, None)
+            return (m.weight, m.bias) if m is not None else (None, None)
+        ts = []
+        for name in ("conv1", "conv2", "lin", "dnn1", "dnn2", "output"):
+            ts += list(wb(name))
+        return ts
+
+    def _native_forward(self, x):
+        if x.dim() != 3:
+            raise RuntimeError(f"SpeechModel expects [B, H, W] input, got {tuple(x.shape)}")
+        if x.dtype != torch.float32:
+            raise RuntimeError(f"expected float32 input, got {x.dtype}")
+        d = self._honk_desc
+        if x.shape[1] != d["height"] or x.shape[2] != d["width"]:
+            raise RuntimeError(f"input {tuple(x.shape[1:])} does not match config ({d['height']}, {d['width']})")
+        x = x.contiguous()
+        lib = _native.load()
+        ts = self._native_tensors()
+        for t in ts:
+            if t is not None and (t.device != x.device or t.dtype != torch.float32):
+                raise RuntimeError(f"honk_amd: parameters must be float32 on {x.device}")
+        ts = [t.detach().contiguous() if t is not None else None for t in ts]
+        desc = _native.CnnDesc(**d)
+        B = x.shape[0]
+        with torch.cuda.device(x.device):
+            out = torch.empty(B, d["n_labels"], dtype=torch.float32, device=x.device)
+            if B == 0:
+                return out
+            ws_bytes = lib.honk_cnn_workspace_bytes(desc, B)
+            if ws_bytes == 0:
+                _native.check(-1, "honk_cnn_workspace_bytes")
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+            _native.check(lib.honk_cnn_forward(desc, _native.ptr_array(ts), x.data_ptr(), out.data_ptr(), B,
+                                               ws.data_ptr(), ws_bytes, _native.stream_handle(x.device)),
+                          "honk_cnn_forward")
+        return out
+
+    def forward(self, x):
+        if _native_ready(x, self):
+            return self._native_forward(x)
+        return self._torch_forward(x)
+
+
+def _pair(v):
+    if isinstance(v, (tuple, list)):
+        return (v[0], v[1])
+    return (v, v)
+
+
+_configs = {
+    ConfigType.CNN_TRAD_POOL2.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=64,
+        n_feature_maps2=64, conv1_size=(20, 8), conv2_size=(10, 4), conv1_pool=(2, 2), conv1_stride=(1, 1),
+        conv2_stride=(1, 1), conv2_pool=(1, 1), tf_variant=True),
+    ConfigType.CNN_ONE_STRIDE1.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=186,
+        conv1_size=(101, 8), conv1_pool=(1, 1), conv1_stride=(1, 1), dnn1_size=128, dnn2_size=128, tf_variant=True),
+    ConfigType.CNN_TSTRIDE2.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=78,
+        n_feature_maps2=78, conv1_size=(16, 8), conv2_size=(9, 4), conv1_pool=(1, 3), conv1_stride=(2, 1),
+        conv2_stride=(1, 1), conv2_pool=(1, 1), dnn1_size=128, dnn2_size=128),
+    ConfigType.CNN_TSTRIDE4.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=100,
+        n_feature_maps2=78, conv1_size=(16, 8), conv2_size=(5, 4), conv1_pool=(1, 3), conv1_stride=(4, 1),
+        conv2_stride=(1, 1), conv2_pool=(1, 1), dnn1_size=128, dnn2_size=128),
+    ConfigType.CNN_TSTRIDE8.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=126,
+        n_feature_maps2=78, conv1_size=(16, 8), conv2_size=(5, 4), conv1_pool=(1, 3), conv1_stride=(8, 1),
+        conv2_stride=(1, 1), conv2_pool=(1, 1), dnn1_size=128, dnn2_size=128),
+    ConfigType.CNN_TPOOL2.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=94,
+        n_feature_maps2=94, conv1_size=(21, 8), conv2_size=(6, 4), conv1_pool=(2, 3), conv1_stride=(1, 1),
+        conv2_stride=(1, 1), conv2_pool=(1, 1), dnn1_size=128, dnn2_size=128),
+    ConfigType.CNN_TPOOL3.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=94,
+        n_feature_maps2=94, conv1_size=(15, 8), conv2_size=(6, 4), conv1_pool=(3, 3), conv1_stride=(1, 1),
+        conv2_stride=(1, 1), conv2_pool=(1, 1), dnn1_size=128, dnn2_size=128),
+    ConfigType.CNN_ONE_FPOOL3.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=54,
+        conv1_size=(101, 8), conv1_pool=(1, 3), conv1_stride=(1, 1), dnn1_size=128, dnn2_size=128),
+    ConfigType.CNN_ONE_FSTRIDE4.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=186,
+        conv1_size=(101, 8), conv1_pool=(1, 1), conv1_stride=(1, 4), dnn1_size=128, dnn2_size=128),
+    ConfigType.CNN_ONE_FSTRIDE8.value: dict(dropout_prob=0.5, height=101, width=40, n_labels=4, n_feature_maps1=336,
+        conv1_size=(101, 8), conv1_pool=(1, 1), conv1_stride=(1, 8), dnn1_size=128, dnn2_size=128),
+    ConfigType.RES15.value: dict(n_labels=12, use_dilation=True, n_layers=13, n_feature_maps=45),
+    ConfigType.RES8.value: dict(n_labels=12, n_layers=6, n_feature_maps=45, res_pool=(4, 3), use_dilation=False),
+    ConfigType.RES26.value: dict(n_labels=12, n_layers=24, n_feature_maps=45, res_pool=(2, 2), use_dilation=False),
+    ConfigType.RES15_NARROW.value: dict(n_labels=12, use_dilation=True, n_layers=13, n_feature_maps=19),
+    ConfigType.RES8_NARROW.value: dict(n_labels=12, n_layers=6, n_feature_maps=19, res_pool=(4, 3),
+                                       use_dilation=False),
+    ConfigType.RES26_NARROW.value: dict(n_labels=12, n_layers=24, n_feature_maps=19, res_pool=(2, 2),
+                                        use_dilation=False),
+}

@@ -1,0 +1,113 @@
+/*
+ * honk_hip.h -- C ABI of libhonk_hip.so, the MI355X (gfx950) forward path of
+ * Honk's keyword-spotting CNNs.
+ *
+ * The reference (ljj7975/honk) is pure PyTorch; its "FFI" for this path is the
+ * nn.Module call made by its callers.  Each entry point below replaces one
+ * reference interface:
+ *
+ *   honk_res_forward  <- SpeechResModel.forward   /root/reference/utils/model.py:104-121
+ *   honk_cnn_forward  <- SpeechModel.forward      /root/reference/utils/model.py:186-205
+ *   honk_res_pack     <- SerializableModule.load  /root/reference/utils/model.py:79-80
+ *                        (state_dict -> kernel layout, done once per weight change)
+ *   honk_*_desc       <- the config dicts          /root/reference/utils/model.py:381-414
+ *
+ * Conventions: every pointer named x/logits/packed/tensors[i]/workspace is a
+ * DEVICE pointer (hipMalloc / torch caching allocator); `stream` is a
+ * hipStream_t passed as void*.  Work is enqueued on `stream`; no call
+ * synchronises, allocates device memory or keeps global mutable state besides a
+ * thread-local last-error string.  Status: 0 = ok, <0 = error, see
+ * honk_last_error().  All arithmetic is IEEE fp32 (fp32 MFMA / FMA).
+ */
+#ifndef HONK_HIP_H
+#define HONK_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HONK_OK 0
+#define HONK_ERR_ARG (-1)        /* bad descriptor / shape / null pointer        */
+#define HONK_ERR_UNSUPPORTED (-2) /* configuration outside the kernels' envelope */
+#define HONK_ERR_WORKSPACE (-3)  /* workspace too small                          */
+#define HONK_ERR_HIP (-4)        /* a HIP runtime call failed                    */
+
+/* ---- SpeechResModel (res8/15/26[-narrow]); utils/model.py:82-121 ------------- */
+typedef struct honk_res_desc {
+  int32_t n_labels;       /* config["n_labels"]                                  */
+  int32_t n_maps;         /* config["n_feature_maps"]   (1..48 supported)        */
+  int32_t n_layers;       /* config["n_layers"]                                  */
+  int32_t use_dilation;   /* config["use_dilation"]: conv{i} dilation 2**((i-1)//3) */
+  int32_t pool_h, pool_w; /* config["res_pool"], or 0,0 when absent              */
+  int32_t height, width;  /* input frames x MFCC coefficients (101, 40)          */
+} honk_res_desc;
+
+/* number of floats of the packed (kernel-layout) weight buffer */
+size_t honk_res_packed_floats(const honk_res_desc* d);
+/* bytes of scratch needed by honk_res_forward for `batch` clips */
+size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch);
+/*
+ * Pack a state_dict into kernel layout.  tensors[] (device, fp32, contiguous),
+ * in this order (n_tensors = 3*n_layers + 3):
+ *   conv0.weight [C,1,3,3], conv1.weight .. conv{L}.weight [C,C,3,3],
+ *   bn1.running_mean, bn1.running_var, .., bn{L}.running_mean, bn{L}.running_var [C],
+ *   output.weight [n_labels,C], output.bias [n_labels]
+ */
+int honk_res_pack(const honk_res_desc* d, const float* const* tensors, int32_t n_tensors,
+                  float* packed, void* stream);
+/* x: [batch, height, width] fp32;  logits: [batch, n_labels] fp32 (eval-mode forward) */
+int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x, float* logits,
+                     int64_t batch, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- SpeechModel (cnn-*); utils/model.py:123-205 ------------------------------ */
+typedef struct honk_cnn_desc {
+  int32_t height, width, n_labels;
+  int32_t c1_out, c1_kh, c1_kw, c1_sh, c1_sw, p1_h, p1_w;   /* conv1 + pool1         */
+  int32_t has_conv2, c2_out, c2_kh, c2_kw, c2_sh, c2_sw, p2_h, p2_w;
+  int32_t has_lin;                                        /* Linear(flat, 32), no ReLU */
+  int32_t dnn1, dnn2;                                     /* 0 = absent              */
+  int32_t dnn1_relu;                                      /* 1 unless tf_variant     */
+} honk_cnn_desc;
+
+size_t honk_cnn_workspace_bytes(const honk_cnn_desc* d, int64_t batch);
+/*
+ * tensors[] (device fp32, contiguous; NULL for absent layers), fixed order of 12:
+ *   conv1.weight, conv1.bias, conv2.weight, conv2.bias, lin.weight, lin.bias,
+ *   dnn1.weight, dnn1.bias, dnn2.weight, dnn2.bias, output.weight, output.bias
+ * No packing: OIHW weights are already the [N][K] operand of the implicit GEMM.
+ */
+int honk_cnn_forward(const honk_cnn_desc* d, const float* const* tensors, const float* x,
+                     float* logits, int64_t batch, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
+/* ---- layer-level operators (used by the cnn driver; exported for tests) ------- */
+/* out[b][n][oh][ow] = act(bias[n] + sum_{ci,kh,kw} in[b][ci][oh*sh+kh][ow*sw+kw] * w[n][ci][kh][kw]) */
+int honk_conv2d_f32(const float* in, const float* w, const float* bias, float* out, int64_t batch,
+                    int32_t cin, int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw,
+                    int32_t sh, int32_t sw, int32_t relu, void* stream);
+/* nn.MaxPool2d((kh,kw)) on NCHW, stride = kernel, floor */
+int honk_maxpool2d_f32(const float* in, float* out, int64_t batch, int32_t c, int32_t h, int32_t w,
+                       int32_t kh, int32_t kw, void* stream);
+/* y[m][n] = act(b[n] + sum_k x[m][k] * w[n][k])  (nn.Linear) */
+int honk_linear_f32(const float* x, const float* w, const float* b, float* y, int64_t m, int32_t k,
+                    int32_t n, int32_t relu, void* stream);
+
+/* ---- diagnostics --------------------------------------------------------------- */
+const char* honk_last_error(void);
+const char* honk_version(void);
+/*
+ * Per-launch timing of the dominant kernel (res block conv) with hipEvents
+ * recorded on the launch stream.  enable=1 starts a window (clears it);
+ * honk_timing_read synchronises the recorded events and returns the summed
+ * kernel time (ms), the launch count and the summed algorithmic FLOP.
+ */
+int honk_timing_enable(int32_t enable);
+int honk_timing_read(double* total_ms, int64_t* launches, double* flop);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HONK_HIP_H */
