@@ -42,7 +42,7 @@ _PROTOS = {
     "honk_cnn_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(CnnDesc), ctypes.c_int64]),
     "honk_cnn_forward": (ctypes.c_int, [ctypes.POINTER(CnnDesc), ctypes.POINTER(ctypes.c_void_p), c_f32p, c_f32p,
                                         ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
-    "honk_conv2d_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 10
+    "honk_conv2d_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 9
                         + [ctypes.c_void_p]),
     "honk_maxpool2d_f32": (ctypes.c_int, [c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 5
                            + [ctypes.c_void_p]),
