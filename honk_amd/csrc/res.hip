@@ -93,11 +93,21 @@ __device__ __forceinline__ void issue_stage(const BlockArgs& a, int tile, int dy
 }
 
 // One (dx, q) step of a stage: reads the A fragments of step K+1 while the
-// MFMAs of step K run.  Template recursion keeps every register index static.
-template <int NT, int MT, int K>
-__device__ __forceinline__ void stage_step(const char* base, const int (&aoff)[3][MT],
-                                           const f32x4 (&bcur)[3][NT], f32x4 (&acc)[MT],
-                                           f32x4 (&a0)[MT], f32x4 (&a1)[MT]) {
+// MFMAs of step K run; after the last q of a dx, that dx's B registers are
+// refilled with the next stage's fragments (row offset NDY) so the L2 latency
+// hides under the remaining MFMAs.  Template recursion keeps register indices static.
+template <int NT>
+__device__ __forceinline__ void load_b_dx(__amdgpu_buffer_rsrc_t wr, int dy, int dx, int lane16, f32x4 (&b)[NT]) {
+#pragma unroll
+  for (int q = 0; q < NT; ++q)
+    b[q] = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, lane16, ((dy * 3 + dx) * NT + q) * 1024, 0));
+}
+
+template <int NT, int MT, int NDY, int K>
+__device__ __forceinline__ void stage_step(const char* base, const int (&aoff)[3][MT], f32x4 (&bcur)[3][NT],
+                                           f32x4 (&acc)[MT], f32x4 (&a0)[MT], f32x4 (&a1)[MT],
+                                           __amdgpu_buffer_rsrc_t wr, int lane16) {
   constexpr int NK = 3 * NT;
   if constexpr (K < NK) {
     constexpr int dx = K / NT, q = K % NT;
@@ -114,19 +124,20 @@ __device__ __forceinline__ void stage_step(const char* base, const int (&aoff)[3
       for (int m = 0; m < MT; ++m)
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[m][j], bcur[dx][q][j], acc[m], 0, 0, 0);
     }
+    if constexpr (q == NT - 1) load_b_dx<NT>(wr, NDY, dx, lane16, bcur[dx]);
     __builtin_amdgcn_sched_barrier(0);
-    stage_step<NT, MT, K + 1>(base, aoff, bcur, acc, a0, a1);
+    stage_step<NT, MT, NDY, K + 1>(base, aoff, bcur, acc, a0, a1, wr, lane16);
   }
 }
 
-template <int NT, int MT>
-__device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff)[3][MT],
-                                              const f32x4 (&bcur)[3][NT], f32x4 (&acc)[MT]) {
+template <int NT, int MT, int NDY>
+__device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff)[3][MT], f32x4 (&bcur)[3][NT],
+                                              f32x4 (&acc)[MT], __amdgpu_buffer_rsrc_t wr, int lane16) {
   const char* base = (const char*)cur;
   f32x4 a0[MT], a1[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) a0[m] = *(const f32x4*)(base + aoff[0][m]);
-  stage_step<NT, MT, 0>(base, aoff, bcur, acc, a0, a1);
+  stage_step<NT, MT, NDY, 0>(base, aoff, bcur, acc, a0, a1, wr, lane16);
 }
 
 // B fragments of the 3 taps of row offset dy: frag[nt][tap][q][lane][4], read
@@ -134,11 +145,7 @@ __device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff
 template <int NT>
 __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t wr, int dy, int lane16, f32x4 (&b)[3][NT]) {
 #pragma unroll
-  for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-    for (int q = 0; q < NT; ++q)
-      b[dx][q] = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, lane16, ((dy * 3 + dx) * NT + q) * 1024, 0));
+  for (int dx = 0; dx < 3; ++dx) load_b_dx<NT>(wr, dy, dx, lane16, b[dx]);
 }
 
 template <int NT, int MT>
@@ -160,8 +167,7 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   }
 
   // B operand: the layer's weights for out-channel tile nt, streamed from L2 one
-  // row offset (3 taps) per stage; the next stage's fragments are loaded right
-  // after this stage's MFMAs and land while the wave waits at the barrier
+  // row offset (3 taps) per stage (refilled inside compute_stage after last use)
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.wfrag + (size_t)nt * 9 * G::Q * 64 * 4), (short)0, 9 * G::Q * 64 * 16, 0x00020000);
   const int lane16 = lane * 16;
@@ -196,6 +202,29 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   int tile = lb;
   if (tile >= a.ntiles) return;
 
+  // per-lane epilogue offset (bytes) within a tile: pixel (mg*MT*16 + g*4), channel cout
+  const int eoff = ((mg * MT * 16 + g * 4) * G::CP + cout) * 4;
+  // buffer descriptor over the valid pixels of `tile` in an NHWC(CP) tensor
+  auto tile_rsrc = [&](const float* t) {
+    const int b = tile / a.nbands;
+    const int h0 = (tile - b * a.nbands) * a.TH;
+    const int vp = min(a.TH, a.H - h0) * a.W;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(t + ((size_t)b * a.H + h0) * a.W * G::CP), (short)0,
+                                             vp * G::CP * 4, 0x00020000);
+  };
+  // residual of this tile, loaded one stage ahead of the epilogue
+  float rv[MT][4];
+  auto prefetch_res = [&]() {
+    if (a.res) {
+      const __amdgpu_buffer_rsrc_t rr = tile_rsrc(a.res);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          rv[m][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, eoff, (m * 16 + r) * G::CP * 4, 0));
+    }
+  };
+
   int s = 0;
   issue_stage<NT, MT>(a, tile, 0, smem, wave, lane);
   while (true) {
@@ -207,14 +236,14 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   {                                                                                     \
     float* cur = smem + (s & 1) * G::BUF;                                               \
     float* nxt = smem + ((s + 1) & 1) * G::BUF;                                         \
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                    \
+    __builtin_amdgcn_s_waitcnt(0); /* all counters: visible to the waitcnt pass */      \
     __syncthreads();                                                                    \
     if (DY < 2)                                                                         \
       issue_stage<NT, MT>(a, tile, DY + 1, nxt, wave, lane);                            \
     else if (tile + GR < a.ntiles)                                                      \
       issue_stage<NT, MT>(a, tile + GR, 0, nxt, wave, lane);                            \
-    compute_stage<NT, MT>(cur, aoff, bcur, acc);                                        \
-    load_b<NT>(wr, (DY + 1) % 3, lane16, bcur); /* lands while waiting at the barrier */ \
+    if (DY == 2) prefetch_res();                                                        \
+    compute_stage<NT, MT, (DY + 1) % 3>(cur, aoff, bcur, acc, wr, lane16);              \
     ++s;                                                                                \
   }
     HONK_STAGE(0)
@@ -224,27 +253,19 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
 
     // epilogue: ReLU (+ residual) -> pre-BN store (even layers) and BN store.
     // C/D layout of 16x16x4: lane holds rows g*4+r (pixels) of column i16 (cout).
+    // Buffer stores past the tile's valid pixels are dropped by the bounds check.
     {
-      const int b = tile / a.nbands;
-      const int h0 = (tile - b * a.nbands) * a.TH;
-      const size_t tbase = ((size_t)b * a.H + h0) * a.W * G::CP;  // wave-uniform
-      int ebase = (mg * MT * 16 + g * 4) * G::CP + cout;
-      int lim = min(a.TH, a.H - h0) * a.W - (mg * MT * 16 + g * 4);
-      asm volatile("" : "+v"(ebase), "+v"(lim));  // keep these from being hoisted/expanded
-      const float* res_t = a.res ? a.res + tbase : nullptr;
-      float* pre_t = a.out_pre ? a.out_pre + tbase : nullptr;
-      float* bn_t = a.out_bn + tbase;
+      const __amdgpu_buffer_rsrc_t bn_r = tile_rsrc(a.out_bn);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (m * 16 + r < lim) {
-            const int idx = ebase + (m * 16 + r) * G::CP;
-            float v = fmaxf(acc[m][r], 0.f);
-            if (res_t) v += res_t[idx];
-            if (pre_t) pre_t[idx] = v;
-            bn_t[idx] = fmaf(v, bsc, bsh);
-          }
+          const int so = (m * 16 + r) * G::CP * 4;
+          float v = fmaxf(acc[m][r], 0.f);
+          if (a.res) v += rv[m][r];
+          if (a.out_pre)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), tile_rsrc(a.out_pre), eoff, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, fmaf(v, bsc, bsh)), bn_r, eoff, so, 0);
         }
       }
     }
@@ -471,7 +492,8 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
 
 static int64_t chunk_clips(const Layout& L, int64_t batch) {
   const size_t per_clip = (size_t)L.H * L.W * L.CP * sizeof(float);
-  int64_t ch = (int64_t)((size_t)3 << 30) / (int64_t)per_clip;  // ~3 GiB per activation buffer
+  // 4096 clips (3.2 GB per buffer for res15) keeps >200 tiles per CU per launch
+  int64_t ch = per_clip <= ((size_t)1 << 20) ? 4096 : (int64_t)((size_t)4 << 30) / (int64_t)per_clip;
   if (const char* e = getenv("HONK_RES_CHUNK")) ch = atoll(e);
   if (ch < 1) ch = 1;
   return batch < ch ? batch : ch;
