@@ -90,6 +90,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from honk_amd import _native
+    from honk_amd import distributed as hd
     from honk_amd import model as hm
     from oracle import ref_numpy as orc
 
@@ -119,11 +120,7 @@ def main():
         barrier()
         kms, nlaunch, kflop = _native.timing_read()
         _native.timing_enable(False)
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = hd.max_over_ranks(t1 - t0, device=dev)  # whole-job time = slowest rank
 
     # top-1 agreement of the GPU logits with the float64 oracle on a few clips
     idx = [0, B // 3, B - 1]

@@ -36,7 +36,6 @@
 
 namespace honk {
 namespace res {
-
 constexpr int MW = 4;  // waves along M per workgroup
 
 template <int NT, int MT>
@@ -47,8 +46,14 @@ struct Geo {
   static constexpr int NWAVES = NT * MW;
   static constexpr int NTHREADS = 64 * NWAVES;
   static constexpr int MP = 16 * MT * MW;     // max pixels per tile
-  static constexpr int ZOFF = ((MP * CP + 255) / 256) * 256;  // zero pixel (floats)
+  static constexpr int ZOFF = MP * CP;        // zero pixel (floats); MP*CP*4 = MT*NWAVES KiB
   static constexpr int BUF = ZOFF + CP;       // floats per LDS stage buffer
+  static constexpr int SCR = 2 * BUF;         // per-wave 16x16 epilogue transpose scratch
+  static constexpr int LDS_FLOATS = SCR + NWAVES * 256;
+  // VMEM ops a wave issues per stage after its glds: B refills (3*NT) and, in
+  // the tile's last stage, residual loads (MT) + pre/BN stores (2*MT)
+  static constexpr int VM_AFTER_GLDS = 3 * NT;
+  static constexpr int VM_AFTER_GLDS_LAST = 3 * NT + 3 * MT;
 };
 
 struct BlockArgs {
@@ -62,10 +67,19 @@ struct BlockArgs {
   int H, W, dil, TH, nbands, ntiles;
 };
 
+// s_waitcnt vmcnt(N) (expcnt/lgkmcnt untouched), visible to the compiler's waitcnt pass
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
 // A-operand staging: one (tile, dy) band of TH rows x W pixels x CP channels,
 // HBM/L2 -> LDS by buffer_load ... lds (16 B per lane, LDS image lane-linear).
-// Rows outside [0, H) get an out-of-range offset: the buffer bounds check
-// returns zeros, which is exactly the reference's zero padding.
+// Every wave issues exactly MT pieces of 1 KiB (the band buffer holds
+// MT*NWAVES KiB), so the barrier's vmcnt count is a compile-time constant.
+// Rows outside [0, H) and pieces past the band get an out-of-range offset: the
+// buffer bounds check returns zeros (= the reference's zero padding).
 template <int NT, int MT>
 __device__ __forceinline__ void issue_stage(const BlockArgs& a, int tile, int dy, float* buf, int wave,
                                             int lane) {
@@ -76,9 +90,10 @@ __device__ __forceinline__ void issue_stage(const BlockArgs& a, int tile, int dy
   __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.in + (size_t)b * clip_floats), (short)0, clip_floats * 4, 0x00020000);
   const int total = a.TH * a.W * G::CH4;
-  const int npieces = (total + 63) >> 6;
   const int rshift = (dy - 1) * a.dil;
-  for (int pc = wave; pc < npieces; pc += G::NWAVES) {
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int pc = wave + i * G::NWAVES;
     const int ci = (pc << 6) + lane;
     const int pix = ci / G::CH4;
     const int ch = ci - pix * G::CH4;
@@ -92,10 +107,7 @@ __device__ __forceinline__ void issue_stage(const BlockArgs& a, int tile, int dy
   }
 }
 
-// One (dx, q) step of a stage: reads the A fragments of step K+1 while the
-// MFMAs of step K run; after the last q of a dx, that dx's B registers are
-// refilled with the next stage's fragments (row offset NDY) so the L2 latency
-// hides under the remaining MFMAs.  Template recursion keeps register indices static.
+// B fragments of tap (dy, dx): frag[nt][tap][q][lane][4] via a buffer descriptor
 template <int NT>
 __device__ __forceinline__ void load_b_dx(__amdgpu_buffer_rsrc_t wr, int dy, int dx, int lane16, f32x4 (&b)[NT]) {
 #pragma unroll
@@ -104,6 +116,10 @@ __device__ __forceinline__ void load_b_dx(__amdgpu_buffer_rsrc_t wr, int dy, int
         f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, lane16, ((dy * 3 + dx) * NT + q) * 1024, 0));
 }
 
+// One (dx, q) step of a stage: reads the A fragments of step K+1 while the
+// MFMAs of step K run; after the last q of a dx, that dx's B registers are
+// refilled with the next stage's fragments (row offset NDY) so the L2 latency
+// hides under the remaining MFMAs.  Template recursion keeps register indices static.
 template <int NT, int MT, int NDY, int K>
 __device__ __forceinline__ void stage_step(const char* base, const int (&aoff)[3][MT], f32x4 (&bcur)[3][NT],
                                            f32x4 (&acc)[MT], f32x4 (&a0)[MT], f32x4 (&a1)[MT],
@@ -140,18 +156,12 @@ __device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff
   stage_step<NT, MT, NDY, 0>(base, aoff, bcur, acc, a0, a1, wr, lane16);
 }
 
-// B fragments of the 3 taps of row offset dy: frag[nt][tap][q][lane][4], read
-// through a buffer descriptor (lane offset in one VGPR, tap/q offset in SGPR).
-template <int NT>
-__device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t wr, int dy, int lane16, f32x4 (&b)[3][NT]) {
-#pragma unroll
-  for (int dx = 0; dx < 3; ++dx) load_b_dx<NT>(wr, dy, dx, lane16, b[dx]);
-}
-
 template <int NT, int MT>
 __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(BlockArgs a) {
   using G = Geo<NT, MT>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * G::BUF];
+  // ONE LDS array (a second __shared__ object can de-pipeline glds waits):
+  // [stage buffer 0 | stage buffer 1 | per-wave transpose scratch]
+  __shared__ __attribute__((aligned(16))) float smem[G::LDS_FLOATS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -160,6 +170,8 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   const int mg = wave / NT;
   const int g = lane >> 4;
   const int i16 = lane & 15;
+  const int t4 = (lane >> 2) & 3;  // epilogue: 16-byte channel chunk
+  const int u4 = lane & 3;         // epilogue: pixel row within the 4-row group
 
   for (int t = tid; t < G::CP; t += G::NTHREADS) {
     smem[G::ZOFF + t] = 0.f;
@@ -172,7 +184,6 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
       (void*)(a.wfrag + (size_t)nt * 9 * G::Q * 64 * 4), (short)0, 9 * G::Q * 64 * 16, 0x00020000);
   const int lane16 = lane * 16;
   f32x4 bcur[3][NT];
-  load_b<NT>(wr, 0, lane16, bcur);
 
   // A operand addresses (bytes within a stage buffer), one per (dx, m-tile)
   const int TP = a.TH * a.W;
@@ -191,9 +202,13 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
     }
   }
 
-  const int cout = nt * 16 + i16;
-  const float bsc = a.bn_scale[cout];
-  const float bsh = a.bn_shift[cout];
+  // epilogue constants: after the 16x16 transpose lane (g, t4, u4) holds pixel
+  // row 4g+u4 of an m-tile, out channels nt*16 + 4*t4 .. +3 (one 16-byte chunk)
+  const int c4 = nt * 16 + 4 * t4;
+  const f32x4 bsc = *(const f32x4*)(a.bn_scale + c4);
+  const f32x4 bsh = *(const f32x4*)(a.bn_shift + c4);
+  const int eoff = ((mg * MT * 16 + 4 * g + u4) * G::CP + c4) * 4;
+  float* scr = smem + G::SCR + wave * 256;
 
   // XCD-aware tile order: blocks sharing an XCD (bid % 8) walk adjacent tiles
   const int GR = gridDim.x;
@@ -202,47 +217,49 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   int tile = lb;
   if (tile >= a.ntiles) return;
 
-  // per-lane epilogue offset (bytes) within a tile: pixel (mg*MT*16 + g*4), channel cout
-  const int eoff = ((mg * MT * 16 + g * 4) * G::CP + cout) * 4;
-  // buffer descriptor over the valid pixels of `tile` in an NHWC(CP) tensor
+  // buffer descriptor over the valid pixels of `tile` in an NHWC(CP) tensor;
+  // a null tensor gets 0 records (loads return 0, stores are dropped)
   auto tile_rsrc = [&](const float* t) {
     const int b = tile / a.nbands;
     const int h0 = (tile - b * a.nbands) * a.TH;
     const int vp = min(a.TH, a.H - h0) * a.W;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(t + ((size_t)b * a.H + h0) * a.W * G::CP), (short)0,
-                                             vp * G::CP * 4, 0x00020000);
-  };
-  // residual of this tile, loaded one stage ahead of the epilogue
-  float rv[MT][4];
-  auto prefetch_res = [&]() {
-    if (a.res) {
-      const __amdgpu_buffer_rsrc_t rr = tile_rsrc(a.res);
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          rv[m][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, eoff, (m * 16 + r) * G::CP * 4, 0));
-    }
+    const size_t off = ((size_t)b * a.H + h0) * a.W * G::CP;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(t ? t + off : a.out_bn), (short)0, t ? vp * G::CP * 4 : 0,
+                                             0x00020000);
   };
 
-  int s = 0;
+  // prologue: stage (tile, dy=0) and its B fragments, fully landed before the loop
   issue_stage<NT, MT>(a, tile, 0, smem, wave, lane);
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) load_b_dx<NT>(wr, 0, dx, lane16, bcur[dx]);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+
+  int s = 0;
+  f32x4 rv[MT];
   while (true) {
     f32x4 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // stage DY: wait for this stage's glds (issued one stage ago) in all waves,
+    // then prefetch the next stage into the other buffer and run the MFMAs
 #define HONK_STAGE(DY)                                                                  \
   {                                                                                     \
     float* cur = smem + (s & 1) * G::BUF;                                               \
     float* nxt = smem + ((s + 1) & 1) * G::BUF;                                         \
-    __builtin_amdgcn_s_waitcnt(0); /* all counters: visible to the waitcnt pass */      \
-    __syncthreads();                                                                    \
+    if (DY == 0) wait_vmcnt<G::VM_AFTER_GLDS_LAST>(); else wait_vmcnt<G::VM_AFTER_GLDS>(); \
+    __builtin_amdgcn_s_barrier();                                                       \
     if (DY < 2)                                                                         \
       issue_stage<NT, MT>(a, tile, DY + 1, nxt, wave, lane);                            \
     else if (tile + GR < a.ntiles)                                                      \
       issue_stage<NT, MT>(a, tile + GR, 0, nxt, wave, lane);                            \
-    if (DY == 2) prefetch_res();                                                        \
+    if (DY == 2) {                                                                      \
+      const __amdgpu_buffer_rsrc_t rr = tile_rsrc(a.res);                               \
+      _Pragma("unroll") for (int m = 0; m < MT; ++m)                                    \
+        rv[m] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(        \
+            rr, eoff, m * 16 * G::CP * 4, 0));                                          \
+    }                                                                                   \
     compute_stage<NT, MT, (DY + 1) % 3>(cur, aoff, bcur, acc, wr, lane16);              \
     ++s;                                                                                \
   }
@@ -251,22 +268,29 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
     HONK_STAGE(2)
 #undef HONK_STAGE
 
-    // epilogue: ReLU (+ residual) -> pre-BN store (even layers) and BN store.
-    // C/D layout of 16x16x4: lane holds rows g*4+r (pixels) of column i16 (cout).
-    // Buffer stores past the tile's valid pixels are dropped by the bounds check.
+    // epilogue: 16x16 transpose of each accumulator tile through this wave's
+    // LDS scratch (C/D layout: lane holds rows g*4+r, column i16), then ReLU,
+    // residual add, pre-BN store (even layers) and BN store, 16 B per lane.
+    // Stores past the tile's valid pixels are dropped by the bounds check.
     {
       const __amdgpu_buffer_rsrc_t bn_r = tile_rsrc(a.out_bn);
+      const __amdgpu_buffer_rsrc_t pre_r = tile_rsrc(a.out_pre);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int so = (m * 16 + r) * G::CP * 4;
-          float v = fmaxf(acc[m][r], 0.f);
-          if (a.res) v += rv[m][r];
-          if (a.out_pre)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), tile_rsrc(a.out_pre), eoff, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, fmaf(v, bsc, bsh)), bn_r, eoff, so, 0);
+        for (int r = 0; r < 4; ++r) scr[(4 * g + r) * 16 + i16] = acc[m][r];
+        const f32x4 d = *(const f32x4*)(scr + (4 * g + u4) * 16 + 4 * t4);
+        f32x4 v, o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[k] = fmaxf(d[k], 0.f) + rv[m][k];
+          o[k] = fmaf(v[k], bsc[k], bsh[k]);
         }
+        const int so = m * 16 * G::CP * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                               pre_r, eoff, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o),
+                                               bn_r, eoff, so, 0);
       }
     }
     tile += GR;
@@ -510,6 +534,7 @@ static Plan plan_block(const Layout& L) {
   const int mts[3] = {4, 5, 6};
   for (int mi = 0; mi < 3; ++mi) {
     const int MT = mts[mi];
+    if (L.NT == 3 && MT > 5) continue;  // VGPR budget at 3 waves/SIMD
     const int MP = 16 * MT * MW;
     const int thmax = MP / L.W;
     if (thmax < 1) continue;
@@ -540,7 +565,7 @@ static int dispatch_block(const Plan& p, const BlockArgs& a, hipStream_t st) {
   if (p.NT == nt && p.MT == mt) return launch_block<nt, mt>(a, st);
   HONK_CASE(1, 4) HONK_CASE(1, 5) HONK_CASE(1, 6)
   HONK_CASE(2, 4) HONK_CASE(2, 5) HONK_CASE(2, 6)
-  HONK_CASE(3, 4) HONK_CASE(3, 5) HONK_CASE(3, 6)
+  HONK_CASE(3, 4) HONK_CASE(3, 5)
 #undef HONK_CASE
   return fail(HONK_ERR_UNSUPPORTED, "no block kernel for NT=%d MT=%d", p.NT, p.MT);
 }

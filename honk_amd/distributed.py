@@ -1,0 +1,68 @@
+"""Multi-GPU execution of the forward path: one process per GPU, batch shards.
+
+The reference has no distributed code (no torch.distributed, no
+DataParallel).  Inference shards embarrassingly: each rank takes
+a contiguous slice of the clips and runs the gfx950 forward on its own device;
+the only cross-rank traffic is one 2-element all-reduce of (correct, total) for
+accuracy, and a scalar MAX for timing.  No collective touches the data path.
+Backend: "nccl" (= RCCL over xGMI on ROCm) for GPU ranks, "gloo" on CPU.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n: int, rank: int, world: int):
+    """Contiguous slice [start, stop) of n items for `rank`; sizes differ by at most 1."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def _ctx():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def sharded_logits(model, x, device=None):
+    """Logits of this rank's shard of x ([N,101,40], any device) -> (start, stop, logits)."""
+    rank, world = _ctx()
+    s, e = shard_bounds(x.shape[0], rank, world)
+    xs = x[s:e]
+    if device is not None:
+        xs = xs.to(device, non_blocking=True)
+    with torch.no_grad():
+        return s, e, model(xs)
+
+
+def sharded_accuracy(model, x, labels, device=None):
+    """Top-1 accuracy of `model` over (x, labels) sharded across ranks.
+
+    Each rank scores its slice; (correct, total) are summed with ONE all-reduce.
+    Returns (accuracy, correct, total) -- identical on every rank.
+    """
+    s, e, logits = sharded_logits(model, x, device)
+    lab = labels[s:e].to(logits.device)
+    counts = torch.tensor([(logits.argmax(1) == lab).sum().item(), e - s], dtype=torch.float64)
+    rank, world = _ctx()
+    if world > 1:
+        backend = dist.get_backend()
+        if backend == "nccl":
+            counts = counts.to(logits.device)
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+    correct, total = counts.tolist()
+    return (correct / total if total else 0.0), int(correct), int(total)
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Max of a host scalar over ranks (the bench's whole-job time)."""
+    rank, world = _ctx()
+    if world == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
