@@ -23,6 +23,11 @@ sys.path.insert(0, REPO)
 METRIC = "1s-clips/sec (whole node) + top-1 acc, res15 12-label Speech Commands"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak (= FP32 vector peak)
 HBM_PEAK_GBS = 8000.0
+WORKLOADS = {
+    "res15": "res15 eval forward (SpeechResModel, 13 dilated 3x3 res layers, 45 maps, 12 labels)",
+    "res8": "res8 eval forward (SpeechResModel, avg-pool 4x3, 6 res layers, 45 maps, 12 labels)",
+    "cnn-trad-pool2": "cnn-trad-pool2 eval forward (SpeechModel, conv 20x8 + maxpool 2x2 + conv 10x4 + linear, 4 labels)",
+}
 
 
 def parse():
@@ -30,7 +35,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--batch", type=int, default=131072, help="clips per GPU per step (C4: 1M over 8 GPUs)")
+    p.add_argument("--batch", type=int, default=None,
+                   help="clips per GPU per step (default: res* 131072 = C4's 1M over 8 GPUs; cnn* 65536 = C2)")
     p.add_argument("--model", default="res15")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -97,7 +103,8 @@ def main():
     cfg = dict(hm.find_config(args.model))
     torch.manual_seed(0)
     model = hm.find_model(args.model)(cfg).eval().to(dev)
-    B = args.batch
+    is_res = args.model.startswith("res")
+    B = args.batch or (131072 if is_res else 65536)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(B, 101, 40, device=dev, generator=g)  # resident in HBM before timing
 
@@ -150,12 +157,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic N(0,1) [B,101,40] fp32 MFCC-shaped input resident in HBM; random-init weights",
-            "config": {"workload": f"{args.model} eval forward (SpeechResModel, 13 dilated 3x3 res layers, 45 maps,"
-                                   f" 12 labels)" if args.model == "res15" else f"{args.model} eval forward",
+            "config": {"workload": WORKLOADS.get(args.model, f"{args.model} eval forward"),
                        "per_gpu_batch": B, "global_batch": world * B,
                        "parallelism": f"batch-shard x{world} (no data-path collective)"},
             "model_tflops": round(value * flop_clip / 1e12, 2),
-            "roofline": {"bound": "mfma", "kernel": "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)",
+            "roofline": {"bound": "mfma",
+                         "kernel": ("honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)" if is_res else
+                                    "honk::cnn::conv_gemm_kernel (implicit-GEMM conv/linear, fp32 MFMA)"),
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,

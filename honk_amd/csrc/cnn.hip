@@ -170,7 +170,9 @@ static int launch_gemm(const GemmArgs& a, hipStream_t st) {
   const int64_t gm = cdiv(a.M, BM);
   if (gm > 0x7fffffff) return fail(HONK_ERR_ARG, "GEMM too large (M=%lld)", (long long)a.M);
   dim3 grid((unsigned)gm, (unsigned)cdiv(a.N, BN));
+  TimedLaunch tl(st, 2.0 * (double)a.M * a.N * a.K);
   hipLaunchKernelGGL(conv_gemm_kernel, grid, dim3(256), 0, st, a);
+  tl.done(st);
   HONK_LAUNCH_CHECK("conv_gemm_kernel");
   return HONK_OK;
 }

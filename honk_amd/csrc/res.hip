@@ -531,8 +531,8 @@ struct Plan {
 static Plan plan_block(const Layout& L) {
   Plan best{L.NT, 4, 1, L.H};
   double best_cost = 1e30;
-  const int mts[3] = {4, 5, 6};
-  for (int mi = 0; mi < 3; ++mi) {
+  const int mts[5] = {5, 4, 6, 3, 2};  // preference order on equal cost
+  for (int mi = 0; mi < 5; ++mi) {
     const int MT = mts[mi];
     if (L.NT == 3 && MT > 5) continue;  // VGPR budget at 3 waves/SIMD
     const int MP = 16 * MT * MW;
@@ -540,8 +540,9 @@ static Plan plan_block(const Layout& L) {
     if (thmax < 1) continue;
     const int nb = (L.H + thmax - 1) / thmax;
     const int th = (L.H + nb - 1) / nb;
-    // cost ~ padded pixels per clip (all m-tiles are computed)
-    const double cost = (double)nb * MP;
+    // cost ~ padded pixels per clip (all m-tiles are computed), plus a per-stage
+    // fixed overhead (barrier + staging issue ~ 2.5k cycles vs 576*MT MFMA cycles)
+    const double cost = (double)nb * MP * (1.0 + 4.3 / MT);
     if (cost < best_cost - 1e-9) {
       best_cost = cost;
       best = Plan{L.NT, MT, th, nb};
@@ -563,9 +564,9 @@ static int launch_block(const BlockArgs& a, hipStream_t st) {
 static int dispatch_block(const Plan& p, const BlockArgs& a, hipStream_t st) {
 #define HONK_CASE(nt, mt) \
   if (p.NT == nt && p.MT == mt) return launch_block<nt, mt>(a, st);
-  HONK_CASE(1, 4) HONK_CASE(1, 5) HONK_CASE(1, 6)
-  HONK_CASE(2, 4) HONK_CASE(2, 5) HONK_CASE(2, 6)
-  HONK_CASE(3, 4) HONK_CASE(3, 5)
+  HONK_CASE(1, 2) HONK_CASE(1, 3) HONK_CASE(1, 4) HONK_CASE(1, 5) HONK_CASE(1, 6)
+  HONK_CASE(2, 2) HONK_CASE(2, 3) HONK_CASE(2, 4) HONK_CASE(2, 5) HONK_CASE(2, 6)
+  HONK_CASE(3, 2) HONK_CASE(3, 3) HONK_CASE(3, 4) HONK_CASE(3, 5)
 #undef HONK_CASE
   return fail(HONK_ERR_UNSUPPORTED, "no block kernel for NT=%d MT=%d", p.NT, p.MT);
 }
