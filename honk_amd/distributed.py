@@ -66,3 +66,30 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def world_info():
+    return _ctx()
+
+
+def broadcast_module(module, src: int = 0, buffers_only: bool = False):
+    """Make every rank's parameters/buffers equal to rank `src`'s (DDP start / broadcast_buffers)."""
+    rank, world = _ctx()
+    if world == 1:
+        return
+    tensors = list(module.buffers()) if buffers_only else list(module.parameters()) + list(module.buffers())
+    for t in tensors:
+        dist.broadcast(t.data, src)
+
+
+def allreduce_grads(flat) -> float:
+    """ONE all-reduce (sum) of the flat gradient bucket (RCCL over xGMI on GPU ranks).
+
+    Returns the scale (1/world) that turns the sum into the DDP mean; the fused
+    SGD kernel applies it, so no extra pass over the bucket is needed.
+    """
+    rank, world = _ctx()
+    if world == 1:
+        return 1.0
+    dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM)
+    return 1.0 / world

@@ -23,7 +23,9 @@ import torch
 import torch.nn as nn
 import torch.utils.data as data
 
+from . import distributed as hd
 from . import model as mod
+from .optim import FlatParams, FlatSGD
 
 
 class ConfigBuilder(object):
@@ -115,9 +117,9 @@ def mod_splits(config):
     return splits.splits(config)
 
 
-def _sgd(model, config, lr):
-    return torch.optim.SGD(model.parameters(), lr=lr, nesterov=config["use_nesterov"],
-                           weight_decay=config["weight_decay"], momentum=config["momentum"])
+def _sgd(flat, config, lr):
+    return FlatSGD(flat, lr=lr, momentum=config["momentum"], weight_decay=config["weight_decay"],
+                   nesterov=config["use_nesterov"])
 
 
 def train(config, datasets=None):
@@ -127,9 +129,20 @@ def train(config, datasets=None):
     (momentum buffers reset, :137-141); dev evaluation every ``dev_every``
     epochs keeps the best model (saved to ``output_file``); the best model is
     evaluated on the test set at the end.
+
+    Optimizer: FlatSGD (torch.optim.SGD semantics over one flat bucket; fused
+    HIP kernel on ROCm).  When torch.distributed is initialised with world > 1
+    this is data-parallel with DDP semantics: each rank
+    draws ``batch_size`` clips per step from its shard of the train set, BN uses
+    per-replica batch statistics with running stats broadcast from rank 0, the
+    gradient bucket is summed with ONE all-reduce and averaged in the SGD kernel.
+    Only rank 0 prints and saves.
     """
+    rank, world = hd.world_info()
+    log = rank == 0
     out_dir = os.path.dirname(os.path.abspath(config["output_file"]))
-    os.makedirs(out_dir, exist_ok=True)
+    if log:
+        os.makedirs(out_dir, exist_ok=True)
     train_set, dev_set, test_set = datasets if datasets is not None else mod_splits(config)
     model = config["model_class"](config)
     if config["input_file"]:
@@ -137,7 +150,9 @@ def train(config, datasets=None):
     if not config["no_cuda"]:
         _select_device(config)
         model.cuda()
-    optimizer = _sgd(model, config, config["lr"][0])
+    hd.broadcast_module(model)
+    flat = FlatParams(model)
+    optimizer = _sgd(flat, config, config["lr"][0])
     schedule_steps = list(config["schedule"])
     schedule_steps.append(np.inf)
     sched_idx = 0
@@ -145,28 +160,40 @@ def train(config, datasets=None):
     max_acc = 0
     best_model = None
 
-    train_loader = data.DataLoader(train_set, batch_size=config["batch_size"], shuffle=True, drop_last=True,
-                                   collate_fn=getattr(train_set, "collate_fn", None))
+    if world > 1:
+        sampler = data.distributed.DistributedSampler(train_set, num_replicas=world, rank=rank, shuffle=True,
+                                                      seed=int(config["seed"]), drop_last=True)
+        train_loader = data.DataLoader(train_set, batch_size=config["batch_size"], sampler=sampler, drop_last=True,
+                                       collate_fn=getattr(train_set, "collate_fn", None))
+    else:
+        sampler = None
+        train_loader = data.DataLoader(train_set, batch_size=config["batch_size"], shuffle=True, drop_last=True,
+                                       collate_fn=getattr(train_set, "collate_fn", None))
     dev_loader = data.DataLoader(dev_set, batch_size=min(len(dev_set), 16), shuffle=False,
                                  collate_fn=getattr(dev_set, "collate_fn", None))
     test_loader = _whole_set_loader(test_set)
     step_no = 0
     for epoch_idx in range(config["n_epochs"]):
+        if sampler is not None:
+            sampler.set_epoch(epoch_idx)
         for model_in, labels in train_loader:
             model.train()
             optimizer.zero_grad()
             if not config["no_cuda"]:
                 model_in, labels = model_in.cuda(), labels.cuda()
+            hd.broadcast_module(model, buffers_only=True)
             scores = model(model_in)
             loss = criterion(scores, labels)
             loss.backward()
-            optimizer.step()
+            optimizer.step(grad_scale=hd.allreduce_grads(flat))
             step_no += 1
             if step_no > schedule_steps[sched_idx]:
                 sched_idx += 1
-                print("changing learning rate to {}".format(config["lr"][sched_idx]))
-                optimizer = _sgd(model, config, config["lr"][sched_idx])
-            print_eval("train step #{}".format(step_no), scores, labels, loss)
+                if log:
+                    print("changing learning rate to {}".format(config["lr"][sched_idx]))
+                optimizer = _sgd(flat, config, config["lr"][sched_idx])
+            if log:
+                print_eval("train step #{}".format(step_no), scores, labels, loss)
 
         if epoch_idx % config["dev_every"] == config["dev_every"] - 1:
             model.eval()
@@ -177,15 +204,21 @@ def train(config, datasets=None):
                         model_in, labels = model_in.cuda(), labels.cuda()
                     scores = model(model_in)
                     loss = criterion(scores, labels)
-                    accs.append(print_eval("dev", scores, labels, loss))
+                    if log:
+                        accs.append(print_eval("dev", scores, labels, loss))
+                    else:
+                        accs.append(((scores.argmax(1) == labels).float().mean()).item())
             avg_acc = np.mean(accs)
-            print("final dev accuracy: {}".format(avg_acc))
+            if log:
+                print("final dev accuracy: {}".format(avg_acc))
             if avg_acc > max_acc:
-                print("saving best model...")
                 max_acc = avg_acc
-                model.save(config["output_file"])
+                if log:
+                    print("saving best model...")
+                    model.save(config["output_file"])
                 best_model = copy.deepcopy(model)
-    evaluate(config, best_model, test_loader)
+    if log:
+        evaluate(config, best_model, test_loader)
 
 
 def default_run_config(output_file=None):

@@ -95,6 +95,16 @@ int honk_maxpool2d_f32(const float* in, float* out, int64_t batch, int32_t c, in
 int honk_linear_f32(const float* x, const float* w, const float* b, float* y, int64_t m, int32_t k,
                     int32_t n, int32_t relu, void* stream);
 
+/* ---- training (data-parallel train(), utils/train.py:99-135) -------------------- */
+/*
+ * One torch.optim.SGD step (dampening 0) over a flat fp32 parameter bucket whose
+ * gradients were summed across ranks; grad_scale = 1/world_size.  momentum_buf
+ * (zero-initialised by the caller, re-zeroed when the reference re-creates its
+ * optimizer at a schedule boundary, train.py:137-141) may be NULL iff momentum == 0.
+ */
+int honk_sgd_step_f32(float* params, const float* grads, float* momentum_buf, int64_t n, float lr,
+                      float momentum, float weight_decay, float grad_scale, int32_t nesterov, void* stream);
+
 /* ---- diagnostics --------------------------------------------------------------- */
 const char* honk_last_error(void);
 const char* honk_version(void);

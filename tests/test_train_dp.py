@@ -1,0 +1,105 @@
+"""train() path: FlatSGD == torch.optim.SGD; data-parallel step (gloo, world 2) ==
+mean of per-shard gradients (DDP semantics)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from honk_amd import distributed as hd
+from honk_amd import model as hm
+from honk_amd.optim import FlatParams, FlatSGD
+
+
+def _model(seed=0, name="res8-narrow"):
+    torch.manual_seed(seed)
+    return hm.find_model(name)(dict(hm.find_config(name)))
+
+
+def _batch(n, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, 101, 40, generator=g), torch.randint(0, 12, (n,), generator=g)
+
+
+@pytest.mark.parametrize("momentum,wd,nesterov", [(0.9, 1e-5, False), (0.9, 1e-3, True), (0.0, 0.0, False)])
+def test_flat_sgd_matches_torch_sgd(momentum, wd, nesterov):
+    a, b = _model(), _model()
+    flat = FlatParams(b)
+    opt_a = torch.optim.SGD(a.parameters(), lr=0.1, momentum=momentum, weight_decay=wd, nesterov=nesterov)
+    opt_b = FlatSGD(flat, lr=0.1, momentum=momentum, weight_decay=wd, nesterov=nesterov)
+    crit = torch.nn.CrossEntropyLoss()
+    for step in range(3):
+        x, y = _batch(6, seed=step)
+        for m, opt in ((a, opt_a), (b, opt_b)):
+            m.train()
+            opt.zero_grad()
+            crit(m(x), y).backward()
+            opt.step()
+    for (k, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7, msg=k)
+
+
+def test_optimizer_recreation_resets_momentum():
+    m = _model()
+    flat = FlatParams(m)
+    opt = FlatSGD(flat, lr=0.1, momentum=0.9)
+    x, y = _batch(4)
+    torch.nn.CrossEntropyLoss()(m.train()(x), y).backward()
+    opt.step()
+    assert opt.buf.abs().sum() > 0
+    opt2 = FlatSGD(flat, lr=0.01, momentum=0.9)
+    assert opt2.buf.abs().sum() == 0
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _dp_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _model(seed=rank)            # deliberately different init: broadcast must fix it
+    hd.broadcast_module(m)
+    flat = FlatParams(m)
+    opt = FlatSGD(flat, lr=0.05, momentum=0.9, weight_decay=1e-5)
+    x, y = _batch(8)
+    s, e = hd.shard_bounds(8, rank, world)
+    m.train()
+    opt.zero_grad()
+    hd.broadcast_module(m, buffers_only=True)
+    torch.nn.CrossEntropyLoss()(m(x[s:e]), y[s:e]).backward()
+    scale = hd.allreduce_grads(flat)
+    out[rank] = (flat.grad.clone().numpy() * scale, None)
+    opt.step(grad_scale=scale)
+    out[rank] = (out[rank][0], flat.data.clone().numpy())
+    dist.destroy_process_group()
+
+
+def test_dp_step_equals_mean_of_shard_grads():
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_dp_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    # single-process reference: grads of each shard separately, averaged (DDP semantics)
+    x, y = _batch(8)
+    grads = []
+    for r in range(2):
+        m = _model(seed=0)
+        m.train()
+        s, e = hd.shard_bounds(8, r, 2)
+        torch.nn.CrossEntropyLoss()(m(x[s:e]), y[s:e]).backward()
+        grads.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]).numpy())
+    mean = (grads[0] + grads[1]) / 2
+    np.testing.assert_allclose(res[0][0], mean, rtol=1e-5, atol=1e-7)
+    np.testing.assert_array_equal(res[0][1], res[1][1])   # ranks stay identical
+    m = _model(seed=0)
+    flat = FlatParams(m)
+    flat.grad.copy_(torch.from_numpy(mean))
+    FlatSGD(flat, lr=0.05, momentum=0.9, weight_decay=1e-5).step()
+    np.testing.assert_allclose(res[0][1], flat.data.numpy(), rtol=1e-6, atol=1e-7)
