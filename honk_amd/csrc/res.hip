@@ -31,7 +31,10 @@
 //                  column zero padding are folded into per-lane LDS addresses
 //                  (an out-of-range column reads a zero pixel kept in LDS); row
 //                  padding comes from the buffer bounds check (reads as 0).
-//   tail_kernel    spatial mean + Linear(C, n_labels) (model.py:119-121)
+//   tail           spatial mean + Linear(C, n_labels) (model.py:119-121): the
+//                  last block layer sums its BN output per channel in the
+//                  epilogue (no activation store); tail_sum_kernel finishes the
+//                  mean and the Linear.
 #include "common.h"
 
 namespace honk {
@@ -64,6 +67,8 @@ struct BlockArgs {
   const float* wfrag;     // [NT][9][Q][64][4] B fragments
   const float* bn_scale;  // [CP]
   const float* bn_shift;  // [CP]
+  float* chsum;           // last layer only: [ntiles][MW][CP] partial channel sums of the
+                          // BN output over valid pixels (fused spatial mean), or nullptr
   int H, W, dil, TH, nbands, ntiles;
 };
 
@@ -156,7 +161,7 @@ __device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff
   stage_step<NT, MT, NDY, 0>(base, aoff, bcur, acc, a0, a1, wr, lane16);
 }
 
-template <int NT, int MT>
+template <int NT, int MT, bool LAST>
 __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(BlockArgs a) {
   using G = Geo<NT, MT>;
   // ONE LDS array (a second __shared__ object can de-pipeline glds waits):
@@ -254,7 +259,7 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
       issue_stage<NT, MT>(a, tile, DY + 1, nxt, wave, lane);                            \
     else if (tile + GR < a.ntiles)                                                      \
       issue_stage<NT, MT>(a, tile + GR, 0, nxt, wave, lane);                            \
-    if (DY == 2) {                                                                      \
+    if (DY == 2 && !LAST) {                                                             \
       const __amdgpu_buffer_rsrc_t rr = tile_rsrc(a.res);                               \
       _Pragma("unroll") for (int m = 0; m < MT; ++m)                                    \
         rv[m] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(        \
@@ -271,12 +276,20 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
     // epilogue: 16x16 transpose of each accumulator tile through this wave's
     // LDS scratch (C/D layout: lane holds rows g*4+r, column i16), then ReLU,
     // residual add, pre-BN store (even layers) and BN store, 16 B per lane.
-    // Stores past the tile's valid pixels are dropped by the bounds check.
+    // Stores past the tile's valid pixels are dropped by the bounds check.  In
+    // the last layer (chsum != nullptr) nothing is stored: the BN output is
+    // summed per channel over the tile's valid pixels instead (fused mean).
     {
-      const __amdgpu_buffer_rsrc_t bn_r = tile_rsrc(a.out_bn);
+      const __amdgpu_buffer_rsrc_t bn_r = tile_rsrc(LAST ? nullptr : a.out_bn);
       const __amdgpu_buffer_rsrc_t pre_r = tile_rsrc(a.out_pre);
+      const int b = tile / a.nbands;
+      const int lim = min(a.TH, a.H - (tile - b * a.nbands) * a.TH) * a.W - (mg * MT * 16 + 4 * g + u4);
+      f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+      const __amdgpu_buffer_rsrc_t rr = tile_rsrc(a.res);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
+        if (LAST)  // last layer: residual loaded here (no prefetch registers)
+          rv[m] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, eoff, m * 16 * G::CP * 4, 0));
 #pragma unroll
         for (int r = 0; r < 4; ++r) scr[(4 * g + r) * 16 + i16] = acc[m][r];
         const f32x4 d = *(const f32x4*)(scr + (4 * g + u4) * 16 + 4 * t4);
@@ -291,6 +304,21 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
                                                pre_r, eoff, so, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o),
                                                bn_r, eoff, so, 0);
+        if (LAST && m * 16 < lim) csum += o;
+      }
+      if (LAST) {
+        // reduce over the 16 lanes holding the same 4 channels (u4: xor 1,2; g: xor 16,32)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float t = csum[k];
+          t += __shfl_xor(t, 1);
+          t += __shfl_xor(t, 2);
+          t += __shfl_xor(t, 16);
+          t += __shfl_xor(t, 32);
+          csum[k] = t;
+        }
+        if ((lane & 0x33) == 0)
+          *(f32x4*)(a.chsum + ((size_t)tile * MW + mg) * G::CP + c4) = csum;
       }
     }
     tile += GR;
@@ -425,6 +453,27 @@ __global__ __launch_bounds__(256) void tail_kernel(const float* __restrict__ x, 
   }
 }
 
+// logits[b] = Wout . (sum of the fused per-tile channel sums) / HW + bout
+__global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ chsum, const float* __restrict__ wout,
+                                                      const float* __restrict__ bout, float* __restrict__ logits,
+                                                      int nparts, int HW, int C, int CP, int NL) {
+  __shared__ float mean[64];
+  const int b = blockIdx.x;
+  const int c = threadIdx.x;
+  if (c < CP) {
+    const float* p = chsum + (size_t)b * nparts * CP + c;
+    float s = 0.f;
+    for (int i = 0; i < nparts; ++i) s += p[(size_t)i * CP];
+    mean[c] = s / (float)HW;
+  }
+  __syncthreads();
+  for (int n = c; n < NL; n += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < C; ++k) acc = fmaf(wout[n * C + k], mean[k], acc);
+    logits[(int64_t)b * NL + n] = acc + bout[n];
+  }
+}
+
 // --------------------------------------------------------------------------- //
 // weight packing
 // --------------------------------------------------------------------------- //
@@ -556,7 +605,10 @@ static int launch_block(const BlockArgs& a, hipStream_t st) {
   using G = Geo<NT, MT>;
   int grid = cu_count();
   if (grid > a.ntiles) grid = a.ntiles;
-  hipLaunchKernelGGL((block_kernel<NT, MT>), dim3(grid), dim3(G::NTHREADS), 0, st, a);
+  if (a.chsum)
+    hipLaunchKernelGGL((block_kernel<NT, MT, true>), dim3(grid), dim3(G::NTHREADS), 0, st, a);
+  else
+    hipLaunchKernelGGL((block_kernel<NT, MT, false>), dim3(grid), dim3(G::NTHREADS), 0, st, a);
   HONK_LAUNCH_CHECK("res block_kernel");
   return HONK_OK;
 }
@@ -608,7 +660,8 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   Layout L;
   if (make_layout(d, &L) != HONK_OK || batch < 1) return 0;
   const int64_t ch = chunk_clips(L, batch);
-  return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float);
+  const Plan p = plan_block(L);
+  return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
 }
 
 int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tensors, float* packed,
@@ -662,6 +715,7 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
   const size_t act = (size_t)chunk * L.H * L.W * L.CP;
   float* R = (float*)workspace;
   float* X[2] = {R + act, R + 2 * act};
+  float* chsum = R + 3 * act;  // [chunk][nbands][MW][CP] fused-mean partial sums
   const Plan p = plan_block(L);
   const double layer_flop_per_clip = 2.0 * L.H * L.W * L.C * L.C * 9;
 
@@ -686,16 +740,23 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
       a.TH = p.TH;
       a.nbands = p.nbands;
       a.ntiles = (int)(n * p.nbands);
+      a.chsum = (i == L.L) ? chsum : nullptr;  // last layer: fused spatial mean, no stores
+      if (i == L.L) a.out_pre = nullptr;
       TimedLaunch tl(st, layer_flop_per_clip * (double)n);
       rc = dispatch_block(p, a, st);
       tl.done(st);
       if (rc) return rc;
     }
-    const float* last = (L.L == 0) ? R : X[(L.L + 1) & 1];
-    hipLaunchKernelGGL(tail_kernel, dim3((unsigned)n), dim3(L.CP * (256 / L.CP)), 0, st, last,
-                       packed + L.off_wout, packed + L.off_bout, logits + c0 * L.NL, L.H * L.W, L.C,
-                       L.CP, L.NL);
-    HONK_LAUNCH_CHECK("res tail_kernel");
+    if (L.L == 0) {  // no block layer: mean of the conv0 output
+      hipLaunchKernelGGL(tail_kernel, dim3((unsigned)n), dim3(L.CP * (256 / L.CP)), 0, st, R,
+                         packed + L.off_wout, packed + L.off_bout, logits + c0 * L.NL, L.H * L.W, L.C,
+                         L.CP, L.NL);
+      HONK_LAUNCH_CHECK("res tail_kernel");
+    } else {
+      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+                         packed + L.off_bout, logits + c0 * L.NL, p.nbands * MW, L.H * L.W, L.C, L.CP, L.NL);
+      HONK_LAUNCH_CHECK("res tail_sum_kernel");
+    }
   }
   return HONK_OK;
 }

@@ -174,7 +174,7 @@ def test_abi_queries_without_gpu():
                         height=101, width=40)
     n = lib.honk_res_packed_floats(d)
     assert n >= 45 * 9 + 13 * 9 * 48 * 48
-    assert lib.honk_res_workspace_bytes(d, 10) == 3 * 10 * 101 * 40 * 48 * 4
+    assert lib.honk_res_workspace_bytes(d, 10) == 3 * 10 * 101 * 40 * 48 * 4 + 10 * 13 * 4 * 48 * 4
     bad = _native.ResDesc(n_labels=12, n_maps=64, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
                           height=101, width=40)
     assert lib.honk_res_packed_floats(bad) == 0
