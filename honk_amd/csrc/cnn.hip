@@ -17,86 +17,123 @@
 namespace honk {
 namespace cnn {
 
-constexpr int BM = 64;   // output pixels per block
+constexpr int BM = 128;  // output pixels per block
 constexpr int BN = 64;   // output channels per block
-constexpr int BK = 16;   // reduction slice per LDS stage
-constexpr int PAD = 4;   // LDS row padding (floats)
+constexpr int BK = 32;   // reduction slice per LDS stage
+constexpr int PADM = 4;  // LDS row padding (floats)
+constexpr int KTAB = 4096;  // max K with an LDS k->offset table (else computed)
 
 struct GemmArgs {
   const float* in;   // NCHW [B][Cin][H][W]
   const float* w;    // [N][K]
   const float* bias; // [N] or nullptr
-  float* out;        // NCHW [B][N][OH][OW]
-  int64_t M;         // B * OH * OW
+  float* out;        // NCHW [B][N][OH][OW], or [B][N][OH/2][OW/2] when pool2 fused
+  int64_t M;         // GEMM rows: B*OH*OW, or B*PH*PW*4 (pool2: 4 window members per pooled pixel)
   int N, K;
   int Cin, H, W, KH, KW, SH, SW, OH, OW;
+  int PH, PW;        // pooled output dims (pool2 fused)
   int relu;
 };
 
-// 256 threads = 4 waves in a 2 (n) x 2 (m) grid; each wave owns a 32x32 output
-// tile = 2x2 MFMA 16x16 tiles.  LDS: Ws[k][n], Xs[k][m], double-buffered via
-// registers (global loads for slice t+1 are issued before the MFMAs of slice t).
+// D[n][m] = act(bias[n] + sum_k W[n][k] * X[k][m]) on v_mfma_f32_16x16x4_f32.
+// 256 threads = 4 waves; wave w owns pixels [32w, 32w+32) of the block's 128
+// (2 m-tiles) and all 64 out channels (4 n-tiles) -> 8 accumulators.  X is
+// gathered from NCHW through a per-block k->offset table in LDS (no integer
+// division in the K loop); W rows are read 16 B at a time.  Slices are staged
+// LDS <- registers with the next slice's global loads in flight during the MFMAs.
+// POOL2: rows are ordered (clip, ph, pw, 2x2 member) so the four members of a
+// max-pool window sit in 4 adjacent lanes: the epilogue max-reduces them with
+// two lane swaps and stores only the pooled value (nn.MaxPool2d((2,2)) fused).
+template <bool POOL2>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
-  __shared__ float Ws[2][BK][BN + PAD];
-  __shared__ float Xs[2][BK][BM + PAD];
+  __shared__ float Ws[2][BK][BN + PADM];
+  __shared__ float Xs[2][BK][BM + PADM];
+  __shared__ int ktab[KTAB];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wn = wave >> 1, wm = wave & 1;
   const int64_t m0 = (int64_t)blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
-  const int OHW = a.OH * a.OW;
   const int KHW = a.KH * a.KW;
-  const int64_t CinHW = (int64_t)a.Cin * a.H * a.W;
+  const bool use_tab = a.K <= KTAB;
+  if (use_tab)
+    for (int k = tid; k < a.K; k += 256) {
+      const int ci = k / KHW, rem = k - ci * KHW;
+      const int kh = rem / a.KW, kw = rem - kh * a.KW;
+      ktab[k] = (ci * a.H + kh) * a.W + kw;
+    }
 
-  // X loads: this thread always stages pixel column mm = tid % 64, rows kk = tid/64 + 4r
-  const int mm = tid & 63;
-  const int kq = tid >> 6;
-  const int64_t mg = m0 + mm;
-  const bool mvalid = mg < a.M;
+  // X staging: thread owns pixel column mm = tid % 128 and rows kk = tid/128 + 2r
+  const int mm = tid & (BM - 1);
+  const int kq = tid >> 7;
+  const int64_t mglob = m0 + mm;
+  const bool mvalid = mglob < a.M;
   int64_t xbase = 0;
   if (mvalid) {
-    const int64_t b = mg / OHW;
-    const int pix = (int)(mg - b * OHW);
-    const int oh = pix / a.OW, ow = pix - oh * a.OW;
-    xbase = b * CinHW + (int64_t)(oh * a.SH) * a.W + ow * a.SW;
+    int oh, ow;
+    int64_t b;
+    if (POOL2) {
+      const int64_t q = mglob >> 2;
+      const int sub = (int)(mglob & 3);
+      const int PHW = a.PH * a.PW;
+      b = q / PHW;
+      const int pp = (int)(q - b * PHW);
+      const int ph = pp / a.PW, pw = pp - ph * a.PW;
+      oh = 2 * ph + (sub >> 1);
+      ow = 2 * pw + (sub & 1);
+    } else {
+      const int OHW = a.OH * a.OW;
+      b = mglob / OHW;
+      const int pix = (int)(mglob - b * OHW);
+      oh = pix / a.OW;
+      ow = pix - oh * a.OW;
+    }
+    xbase = b * ((int64_t)a.Cin * a.H * a.W) + (int64_t)(oh * a.SH) * a.W + ow * a.SW;
   }
-  // W loads: thread stages rows nn = tid/16 + 16r, column kk = tid % 16
-  const int wk = tid & 15;
-  const int wr = tid >> 4;
+  // W staging: thread owns row n = tid/4, columns (tid%4)*8 .. +7
+  const int wn_row = tid >> 2;
+  const int wk0 = (tid & 3) * 8;
+  const bool wvec = (a.K & 3) == 0 && ((((uintptr_t)a.w) & 15) == 0);
 
-  float xr[4], wv[4];
+  float xr[16], wv[8];
+  auto koffset = [&](int k) -> int {
+    if (use_tab) return ktab[k];
+    const int ci = k / KHW, rem = k - ci * KHW;
+    const int kh = rem / a.KW, kw = rem - kh * a.KW;
+    return (ci * a.H + kh) * a.W + kw;
+  };
   auto load_slice = [&](int k0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = k0 + kq + 4 * r;
-      float v = 0.f;
-      if (mvalid && k < a.K) {
-        const int ci = k / KHW;
-        const int rem = k - ci * KHW;
-        const int kh = rem / a.KW, kw = rem - kh * a.KW;
-        v = a.in[xbase + (int64_t)ci * a.H * a.W + kh * a.W + kw];
-      }
-      xr[r] = v;
-      const int n = n0 + wr + 16 * r;
-      const int kk = k0 + wk;
-      wv[r] = (n < a.N && kk < a.K) ? a.w[(int64_t)n * a.K + kk] : 0.f;
+    for (int r = 0; r < 16; ++r) {
+      const int k = k0 + kq + 2 * r;
+      xr[r] = (mvalid && k < a.K) ? a.in[xbase + koffset(k)] : 0.f;
+    }
+    const int n = n0 + wn_row;
+    const int kb = k0 + wk0;
+    if (n < a.N && wvec && kb + 8 <= a.K) {
+      const f32x4 u = *(const f32x4*)(a.w + (int64_t)n * a.K + kb);
+      const f32x4 v = *(const f32x4*)(a.w + (int64_t)n * a.K + kb + 4);
+      wv[0] = u[0]; wv[1] = u[1]; wv[2] = u[2]; wv[3] = u[3];
+      wv[4] = v[0]; wv[5] = v[1]; wv[6] = v[2]; wv[7] = v[3];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wv[j] = (n < a.N && kb + j < a.K) ? a.w[(int64_t)n * a.K + kb + j] : 0.f;
     }
   };
   auto store_slice = [&](int buf) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      Xs[buf][kq + 4 * r][mm] = xr[r];
-      Ws[buf][wk][wr + 16 * r] = wv[r];
-    }
+    for (int r = 0; r < 16; ++r) Xs[buf][kq + 2 * r][mm] = xr[r];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Ws[buf][wk0 + j][wn_row] = wv[j];
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  __syncthreads();  // ktab ready
   const int nslices = (a.K + BK - 1) / BK;
   load_slice(0);
   store_slice(0);
@@ -107,13 +144,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
       const int kk = ks * 4 + (lane >> 4);
-      float av[2], bv[2];
+      float av[4], bv[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) av[i] = Ws[buf][kk][wn * 32 + i * 16 + (lane & 15)];
+      for (int i = 0; i < 4; ++i) av[i] = Ws[buf][kk][i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bv[j] = Xs[buf][kk][wm * 32 + j * 16 + (lane & 15)];
+      for (int j = 0; j < 2; ++j) bv[j] = Xs[buf][kk][wave * 32 + j * 16 + (lane & 15)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
@@ -125,20 +162,35 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
   // epilogue: D[n][m]; lane holds rows n = (lane>>4)*4 + r, column m = lane & 15
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int64_t m = m0 + wm * 32 + j * 16 + (lane & 15);
-    if (m >= a.M) continue;
-    const int64_t b = m / OHW;
-    const int pix = (int)(m - b * OHW);
-    float* ob = a.out + b * (int64_t)a.N * OHW + pix;
+    const int64_t m = m0 + wave * 32 + j * 16 + (lane & 15);
+    const bool mok = m < a.M;
+    int64_t obase;
+    int64_t plane;
+    if (POOL2) {
+      const int64_t q = m >> 2;
+      const int PHW = a.PH * a.PW;
+      const int64_t b = q / PHW;
+      obase = b * (int64_t)a.N * PHW + (q - b * PHW);
+      plane = PHW;
+    } else {
+      const int OHW = a.OH * a.OW;
+      const int64_t b = m / OHW;
+      obase = b * (int64_t)a.N * OHW + (m - b * OHW);
+      plane = OHW;
+    }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * 32 + i * 16 + (lane >> 4) * 4 + r;
-        if (n < a.N) {
-          float v = acc[i][j][r] + (a.bias ? a.bias[n] : 0.f);
-          if (a.relu) v = fmaxf(v, 0.f);
-          ob[(int64_t)n * OHW] = v;
+        const int n = n0 + i * 16 + (lane >> 4) * 4 + r;
+        float v = acc[i][j][r] + ((a.bias && n < a.N) ? a.bias[n] : 0.f);
+        if (a.relu) v = fmaxf(v, 0.f);
+        if (POOL2) {  // max over the 2x2 window = lanes l, l^1, l^2, l^3 (same n)
+          v = fmaxf(v, __shfl_xor(v, 1));
+          v = fmaxf(v, __shfl_xor(v, 2));
+          if ((lane & 3) == 0 && mok && n < a.N) a.out[obase + (int64_t)n * plane] = v;
+        } else if (mok && n < a.N) {
+          a.out[obase + (int64_t)n * plane] = v;
         }
       }
     }
@@ -165,20 +217,24 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ 
   out[i] = m;
 }
 
-static int launch_gemm(const GemmArgs& a, hipStream_t st) {
+static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return HONK_OK;
   const int64_t gm = cdiv(a.M, BM);
   if (gm > 0x7fffffff) return fail(HONK_ERR_ARG, "GEMM too large (M=%lld)", (long long)a.M);
   dim3 grid((unsigned)gm, (unsigned)cdiv(a.N, BN));
   TimedLaunch tl(st, 2.0 * (double)a.M * a.N * a.K);
-  hipLaunchKernelGGL(conv_gemm_kernel, grid, dim3(256), 0, st, a);
+  if (pool2)
+    hipLaunchKernelGGL((conv_gemm_kernel<true>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<false>), grid, dim3(256), 0, st, a);
   tl.done(st);
   HONK_LAUNCH_CHECK("conv_gemm_kernel");
   return HONK_OK;
 }
 
 static int conv(const float* in, const float* w, const float* bias, float* out, int64_t batch, int cin,
-                int h, int wd, int cout, int kh, int kw, int sh, int sw, int relu, hipStream_t st) {
+                int h, int wd, int cout, int kh, int kw, int sh, int sw, int relu, hipStream_t st,
+                bool pool2 = false) {
   if (kh > h || kw > wd || sh < 1 || sw < 1 || cin < 1 || cout < 1)
     return fail(HONK_ERR_ARG, "bad conv geometry (cin=%d %dx%d k=%dx%d s=%dx%d)", cin, h, wd, kh, kw, sh, sw);
   GemmArgs a;
@@ -186,11 +242,14 @@ static int conv(const float* in, const float* w, const float* bias, float* out, 
   a.Cin = cin; a.H = h; a.W = wd; a.KH = kh; a.KW = kw; a.SH = sh; a.SW = sw;
   a.OH = (h - kh) / sh + 1;
   a.OW = (wd - kw) / sw + 1;
-  a.M = batch * a.OH * a.OW;
+  a.PH = a.OH / 2;
+  a.PW = a.OW / 2;
+  a.M = pool2 ? batch * a.PH * a.PW * 4 : batch * a.OH * a.OW;
   a.N = cout;
   a.K = cin * kh * kw;
   a.relu = relu;
-  return launch_gemm(a, st);
+  if (pool2 && (a.PH < 1 || a.PW < 1)) return fail(HONK_ERR_ARG, "pool larger than conv output");
+  return launch_gemm(a, pool2, st);
 }
 
 static int linear(const float* x, const float* w, const float* b, float* y, int64_t m, int k, int n,
@@ -325,24 +384,26 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
     const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
     const float* xin = x + c0 * d->height * d->width;
     // conv1 + ReLU (model.py:187) -> A ; pool1 (:189) -> B (skip when 1x1)
+    const bool fuse1 = d->p1_h == 2 && d->p1_w == 2;  // conv1 + ReLU + MaxPool2d(2,2) in one kernel
     rc = conv(xin, t[0], t[1], A, n, 1, d->height, d->width, d->c1_out, d->c1_kh, d->c1_kw, d->c1_sh, d->c1_sw, 1,
-              st);
+              st, fuse1);
     if (rc) return rc;
     const float* cur = A;
     float* other = B;
-    if (d->p1_h * d->p1_w > 1) {
+    if (!fuse1 && d->p1_h * d->p1_w > 1) {
       rc = maxpool(A, B, n * d->c1_out, s.oh1, s.ow1, d->p1_h, d->p1_w, st);
       if (rc) return rc;
       cur = B;
       other = A;
     }
     if (d->has_conv2) {  // model.py:190-193
+      const bool fuse2 = d->p2_h == 2 && d->p2_w == 2;
       rc = conv(cur, t[2], t[3], other, n, d->c1_out, s.ph1, s.pw1, d->c2_out, d->c2_kh, d->c2_kw, d->c2_sh,
-                d->c2_sw, 1, st);
+                d->c2_sw, 1, st, fuse2);
       if (rc) return rc;
       const float* c2 = other;
       float* o2 = (float*)cur;
-      if (d->p2_h * d->p2_w > 1) {
+      if (!fuse2 && d->p2_h * d->p2_w > 1) {
         rc = maxpool(c2, o2, n * d->c2_out, s.oh2, s.ow2, d->p2_h, d->p2_w, st);
         if (rc) return rc;
         cur = o2;
