@@ -50,6 +50,8 @@ _PROTOS = {
                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "honk_sgd_step_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64, ctypes.c_float, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p]),
+    "honk_mfcc_f32": (ctypes.c_int, [c_f32p, ctypes.c_int64, ctypes.c_int32, c_f32p, ctypes.c_int32, ctypes.c_int32,
+                                     c_f32p, ctypes.c_int32, c_f32p, ctypes.c_int32, c_f32p, ctypes.c_void_p]),
     "honk_last_error": (ctypes.c_char_p, []),
     "honk_version": (ctypes.c_char_p, []),
     "honk_timing_enable": (ctypes.c_int, [ctypes.c_int32]),

@@ -1,8 +1,10 @@
 """MFCC front-end: numpy restatement of AudioPreprocessor.compute_mfccs
 (/root/reference/utils/manage_audio.py:18-42, librosa 0.6.x semantics).
 
-This is the step before the hot path.  librosa is not
-available in this image, so parity of this module is UNPINNED: it restates the
+This is the step before the hot path.  CPU path: numpy
+below; ROCm path: ``compute_mfccs_batch`` -> ``honk_mfcc_f32`` (csrc/mfcc.hip).
+librosa is not available in this image, so parity of this module is UNPINNED
+(checked against the independent float64 restatement oracle/mfcc_ref.py): it restates the
 published librosa 0.6 algorithms (STFT with centre/reflect padding and a
 periodic Hann window, power spectrum, Slaney mel filterbank with area
 normalisation, ``log`` of the positive entries, a 40x40 DCT-II basis from
@@ -83,3 +85,35 @@ class AudioPreprocessor(object):
         data[pos] = np.log(data[pos])
         out = (self.dct_filters @ data).T  # (frames, n_dct)
         return np.asfortranarray(out[:, :, None]).astype(np.float32)
+
+    # -- batched GPU path (libhonk_hip.so honk_mfcc_f32) ---------------------------
+    def _device_tables(self, device):
+        import torch
+        key = str(device)
+        cache = getattr(self, "_dev_tables", {})
+        if key not in cache:
+            cache[key] = tuple(torch.from_numpy(np.ascontiguousarray(t, dtype=np.float32)).to(device)
+                               for t in (self._window, self._mel, self.dct_filters))
+            self._dev_tables = cache
+        return cache[key]
+
+    def compute_mfccs_batch(self, pcm):
+        """pcm: torch float32 [B, samples] on a ROCm device -> [B, frames, n_dct] (model input layout)."""
+        import torch
+        from . import _native
+        if not pcm.is_cuda:
+            return torch.from_numpy(np.stack([self.compute_mfccs(p.numpy()).squeeze(2) for p in pcm]))
+        pcm = pcm.contiguous().float()
+        B, S = pcm.shape
+        win, mel, dct = self._device_tables(pcm.device)
+        frames = 1 + S // self.hop_length
+        out = torch.empty(B, frames, dct.shape[0], dtype=torch.float32, device=pcm.device)
+        lib = _native.load()
+        with torch.cuda.device(pcm.device):
+            for s0 in range(0, B, 65535):
+                n = min(65535, B - s0)
+                _native.check(lib.honk_mfcc_f32(pcm[s0:].data_ptr(), n, S, win.data_ptr(), self.n_fft,
+                                                self.hop_length, mel.data_ptr(), mel.shape[0], dct.data_ptr(),
+                                                dct.shape[0], out[s0:].data_ptr(), _native.stream_handle(pcm.device)),
+                              "honk_mfcc_f32")
+        return out

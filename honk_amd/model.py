@@ -87,7 +87,22 @@ class SerializableModule(nn.Module):
 
     def load(self, filename):
         # weights_only load: a state_dict holds tensors only
-        self.load_state_dict(torch.load(filename, map_location=lambda storage, loc: storage, weights_only=True))
+        sd = torch.load(filename, map_location=lambda storage, loc: storage, weights_only=True)
+        self.load_state_dict(upgrade_state_dict(self, sd))
+
+
+def upgrade_state_dict(module, sd):
+    """Accept honk-models checkpoints from torch < 0.4.1 (SURVEY §7 'Old checkpoints'):
+    they lack ``bn*.num_batches_tracked``; those buffers only count eval-irrelevant
+    training steps, so they are filled with 0 (what BatchNorm itself does for
+    version-1 state_dicts).  Any other missing/unexpected key still fails strictly."""
+    own = module.state_dict()
+    missing = [k for k in own if k not in sd]
+    if missing and all(k.endswith("num_batches_tracked") for k in missing):
+        sd = dict(sd)
+        for k in missing:
+            sd[k] = torch.zeros_like(own[k])
+    return sd
 
 
 def _native_ready(x, module):

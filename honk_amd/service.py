@@ -68,29 +68,41 @@ class TorchLabelService(LabelService):
         self.model.load(self.model_filename)
         self.model.eval()
 
-    def _features(self, wav_data):
-        pcm = np.frombuffer(wav_data, dtype=np.int16) / 32768.
-        return self.audio_processor.compute_mfccs(pcm).squeeze(2)
+    def _model_input(self, windows):
+        """int16 PCM byte windows -> [B, frames, 40] MFCC on the model's device.
+
+        ROCm: one batched honk_mfcc_f32 launch (csrc/mfcc.hip); CPU: numpy."""
+        pcm = np.stack([np.frombuffer(w, dtype=np.int16) for w in windows]).astype(np.float32) / 32768.
+        if self.no_cuda:
+            return torch.from_numpy(np.stack([self.audio_processor.compute_mfccs(p).squeeze(2) for p in pcm]))
+        return self.audio_processor.compute_mfccs_batch(torch.from_numpy(pcm).cuda())
 
     def label(self, wav_data):
         """Labels audio data as one of the trained labels -> (most likely label, probability)."""
-        model_in = torch.from_numpy(self._features(wav_data)).unsqueeze(0)
-        if not self.no_cuda:
-            model_in = model_in.cuda()
+        model_in = self._model_input([wav_data])
         with torch.no_grad():
             predictions = F.softmax(self.model(model_in).squeeze(0).cpu(), dim=0).numpy()
         return (self.labels[np.argmax(predictions)], np.max(predictions))
 
     def label_batch(self, windows):
-        """All windows of a request in ONE forward; returns [(label, prob)] in window order."""
+        """All windows of a request in ONE MFCC launch + ONE forward; [(label, prob)] in order."""
         if not windows:
             return []
-        x = torch.from_numpy(np.stack([self._features(w) for w in windows]))
-        if not self.no_cuda:
-            x = x.cuda()
         with torch.no_grad():
-            p = F.softmax(self.model(x).cpu(), dim=1).numpy()
+            p = F.softmax(self.model(self._model_input(windows)).cpu(), dim=1).numpy()
         return [(self.labels[int(np.argmax(r))], float(np.max(r))) for r in p]
+
+    def listen(self, wav_data, stride_size_ms=500, method="labels", keyword="command", min_keyword_prob=0.85):
+        """Batched form of server.py:99-112 (ListenEndpoint.POST): 1 s windows every
+        ``stride_size_ms``; returns {label: summed prob} or, for "command_tagging",
+        {"contains_command": bool} with the reference's early-exit order."""
+        windows = list(stride(wav_data, int(2 * 16000 * stride_size_ms / 1000), 2 * 16000))
+        labels = {}
+        for label, prob in self.label_batch(windows):
+            labels[label] = labels.get(label, 0.0) + float(prob)
+            if label == keyword and prob >= min_keyword_prob and method == "command_tagging":
+                return dict(contains_command=True)
+        return dict(contains_command=False) if method == "command_tagging" else labels
 
 
 def stride(array, stride_size, window_size):

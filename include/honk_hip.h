@@ -95,6 +95,18 @@ int honk_maxpool2d_f32(const float* in, float* out, int64_t batch, int32_t c, in
 int honk_linear_f32(const float* x, const float* w, const float* b, float* y, int64_t m, int32_t k,
                     int32_t n, int32_t relu, void* stream);
 
+/* ---- MFCC front-end (AudioPreprocessor.compute_mfccs, utils/manage_audio.py:30-42) ---- */
+/*
+ * pcm [batch][samples] f32 -> out [batch][1 + samples/hop][n_dct] f32 (the
+ * [B,101,40] model input for 1 s @ 16 kHz, hop 160, n_fft 480, 40 mels/DCT).
+ * window [n_fft], mel_weights [n_mels][n_fft/2+1], dct [n_dct][n_mels] are the
+ * librosa-0.6 Hann window / Slaney mel basis / DCT basis (device, f32).
+ * Centre reflect padding, power spectrum, log of positive entries.  batch <= 65535.
+ */
+int honk_mfcc_f32(const float* pcm, int64_t batch, int32_t samples, const float* window, int32_t n_fft,
+                  int32_t hop, const float* mel_weights, int32_t n_mels, const float* dct, int32_t n_dct,
+                  float* out, void* stream);
+
 /* ---- training (data-parallel train(), utils/train.py:99-135) -------------------- */
 /*
  * One torch.optim.SGD step (dampening 0) over a flat fp32 parameter bucket whose

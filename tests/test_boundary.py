@@ -190,3 +190,20 @@ def test_missing_extension_fails_loudly():
             _native.load("/nonexistent/libhonk_hip.so")
     finally:
         _native._lib = saved
+
+
+def test_legacy_checkpoint_without_num_batches_tracked(tmp_path):
+    cfg, params, x, logits, meta = load_fixture("res15")
+    legacy = {k: torch.from_numpy(np.asarray(v)) for k, v in params.items() if not k.endswith("num_batches_tracked")}
+    fn = str(tmp_path / "legacy.pt")
+    torch.save(legacy, fn)
+    m = hm.find_model("res15")(cfg)
+    m.load(fn)
+    with torch.no_grad():
+        out = m.eval()(torch.from_numpy(x)).numpy()
+    np.testing.assert_allclose(out, logits, atol=1e-5, rtol=1e-5)
+    bad = dict(legacy)
+    bad.pop("conv3.weight")
+    torch.save(bad, fn)
+    with pytest.raises(RuntimeError):
+        hm.find_model("res15")(cfg).load(fn)
