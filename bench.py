@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--model", default="res15")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--e2e", action="store_true",
+                   help="serving pipeline: int16-scaled PCM [B,16000] in HBM -> GPU MFCC -> model -> logits")
     p.add_argument("--train", action="store_true",
                    help="C5: data-parallel training step (fwd+bwd, one RCCL all-reduce, fused SGD)")
     return p.parse_args()
@@ -174,17 +176,26 @@ def main():
     B = args.batch or (131072 if is_res else 65536)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(B, 101, 40, device=dev, generator=g)  # resident in HBM before timing
+    step_fn = model
+    if args.e2e:  # raw 1 s PCM windows instead of MFCC maps; MFCC runs on the GPU inside the step
+        from honk_amd.audio import AudioPreprocessor
+        ap = AudioPreprocessor()
+        pcm = (torch.rand(B, 16000, device=dev, generator=g) * 2 - 1) * 0.3
+        x = pcm
+
+        def step_fn(p):
+            return model(ap.compute_mfccs_batch(p))
 
     with torch.no_grad():
         for _ in range(args.warmup):
-            model(x)
+            step_fn(x)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         _native.timing_enable(True)
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            out = model(x)
+            out = step_fn(x)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         barrier()
@@ -194,7 +205,7 @@ def main():
 
     # top-1 agreement of the GPU logits with the float64 oracle on a few clips
     idx = [0, B // 3, B - 1]
-    xs = x[idx].cpu().numpy()
+    xs = (ap.compute_mfccs_batch(x[idx]) if args.e2e else x[idx]).cpu().numpy()
     ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()},
                       cfg, xs)
     got = out[idx].cpu().numpy()
@@ -220,7 +231,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic N(0,1) [B,101,40] fp32 MFCC-shaped input resident in HBM; random-init weights",
-            "config": {"workload": WORKLOADS.get(args.model, f"{args.model} eval forward"),
+            "config": {"workload": ("PCM -> GPU MFCC -> " if args.e2e else "")
+                                   + WORKLOADS.get(args.model, f"{args.model} eval forward"),
                        "per_gpu_batch": B, "global_batch": world * B,
                        "parallelism": f"batch-shard x{world} (no data-path collective)"},
             "model_tflops": round(value * flop_clip / 1e12, 2),
