@@ -23,6 +23,7 @@ sys.path.insert(0, REPO)
 METRIC = "1s-clips/sec (whole node) + top-1 acc, res15 12-label Speech Commands"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak (= FP32 vector peak)
 HBM_PEAK_GBS = 8000.0
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 WORKLOADS = {
     "res15": "res15 eval forward (SpeechResModel, 13 dilated 3x3 res layers, 45 maps, 12 labels)",
     "res8": "res8 eval forward (SpeechResModel, avg-pool 4x3, 6 res layers, 45 maps, 12 labels)",
@@ -40,6 +41,9 @@ def parse():
     p.add_argument("--model", default="res15")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--precision", default="f32", choices=["f32", "bf16"],
+                   help="res path arithmetic: f32 (exact, 1e-4 parity) or bf16 (top-1 parity)")
+    p.add_argument("--no-alt", action="store_true", help="skip the extra bf16-mode measurement of res models")
     p.add_argument("--e2e", action="store_true",
                    help="serving pipeline: int16-scaled PCM [B,16000] in HBM -> GPU MFCC -> model -> logits")
     p.add_argument("--train", action="store_true",
@@ -141,6 +145,42 @@ def train_bench(args, dev, rank, world, barrier):
               flush=True)
 
 
+def measure_alt_bf16(model, x, args, dev, barrier, hd, _native, orc, cfg, B, world):
+    model.honk_precision = "bf16"
+    with torch.no_grad():
+        for _ in range(max(1, args.warmup)):
+            model(x)
+        torch.cuda.synchronize()
+        barrier()
+        _native.timing_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = model(x)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier()
+        kms, nl, kfl = _native.timing_read()
+        _native.timing_enable(False)
+    model.honk_precision = "f32"
+    el = hd.max_over_ranks(t1 - t0, device=dev)
+    idx = list(range(0, B, max(1, B // 32)))[:32]
+    ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}, cfg,
+                      x[idx].cpu().numpy())
+    got = out[idx].cpu().numpy()
+    ach = (kfl / max(nl, 1)) / ((kms / max(nl, 1)) * 1e-3) / 1e12 if nl else None
+    return {"value": round(world * B * args.steps / el, 1), "unit": "clips/s", "dtype": "bf16",
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "roofline": {"bound": "mfma", "kernel": "honk::res::block16_kernel (dilated 3x3 conv, bf16 MFMA)",
+                         "achieved": round(ach, 2) if ach else None, "peak": BF16_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4) if ach else None,
+                         "avg_launch_ms": round(kms / max(nl, 1), 4)},
+            "parity": {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
+                       "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()),
+                       "sample_clips": len(idx)},
+            "note": "bf16 activations/weights, fp32 accumulation; reduced precision vs the fp32 reference, "
+                    "so reported beside the fp32 headline (value), not as it"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -172,6 +212,8 @@ def main():
     cfg = dict(hm.find_config(args.model))
     torch.manual_seed(0)
     model = hm.find_model(args.model)(cfg).eval().to(dev)
+    if args.model.startswith("res"):
+        model.honk_precision = args.precision
     is_res = args.model.startswith("res")
     B = args.batch or (131072 if is_res else 65536)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -203,14 +245,22 @@ def main():
         _native.timing_enable(False)
     elapsed = hd.max_over_ranks(t1 - t0, device=dev)  # whole-job time = slowest rank
 
+    bf16 = is_res and args.precision == "bf16"
+    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
     # top-1 agreement of the GPU logits with the float64 oracle on a few clips
-    idx = [0, B // 3, B - 1]
+    idx = [0, B // 3, B - 1] if not bf16 else list(range(0, B, max(1, B // 32)))[:32]
     xs = (ap.compute_mfccs_batch(x[idx]) if args.e2e else x[idx]).cpu().numpy()
     ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()},
                       cfg, xs)
     got = out[idx].cpu().numpy()
     top1 = float(np.mean(np.argmax(ref, 1) == np.argmax(got, 1)))
     maxerr = float(np.abs(ref - got).max())
+
+    # secondary measurement: the same workload in the bf16 precision mode (C3/C4),
+    # reported beside -- never instead of -- the fp32 headline
+    alt = None
+    if is_res and args.precision == "f32" and not args.no_alt and not args.e2e:
+        alt = measure_alt_bf16(model, x, args, dev, barrier, hd, _native, orc, cfg, B, world)
 
     total = world * B * args.steps
     value = total / elapsed
@@ -229,7 +279,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "bf16" if (is_res and args.precision == "bf16") else "f32",
             "data": "synthetic N(0,1) [B,101,40] fp32 MFCC-shaped input resident in HBM; random-init weights",
             "config": {"workload": ("PCM -> GPU MFCC -> " if args.e2e else "")
                                    + WORKLOADS.get(args.model, f"{args.model} eval forward"),
@@ -237,17 +287,20 @@ def main():
                        "parallelism": f"batch-shard x{world} (no data-path collective)"},
             "model_tflops": round(value * flop_clip / 1e12, 2),
             "roofline": {"bound": "mfma",
-                         "kernel": ("honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)" if is_res else
+                         "kernel": (("honk::res::block16_kernel (dilated 3x3 conv, bf16 MFMA)" if bf16 else
+                                     "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)") if is_res else
                                     "honk::cnn::conv_gemm_kernel (implicit-GEMM conv/linear, fp32 MFMA)"),
                          "achieved": round(achieved, 2) if achieved else None,
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+                         "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4) if achieved else None,
                          "traffic": load_traffic(),
                          "launches": nlaunch, "avg_launch_ms": round(avg_ms, 4),
                          "flop_per_launch": kflop / max(nlaunch, 1)},
             "parity": {"top1_agreement_vs_oracle": top1, "max_abs_logit_err_vs_oracle_f64": maxerr,
                        "sample_clips": len(idx)},
         }
+        if alt is not None:
+            res["bf16_mode"] = alt
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         print(json.dumps(res), flush=True)

@@ -19,7 +19,10 @@ c_f32p = ctypes.c_void_p
 class ResDesc(ctypes.Structure):
     """honk_res_desc -- mirrors the SpeechResModel config keys (utils/model.py:85-92)."""
     _fields_ = [(n, ctypes.c_int32) for n in (
-        "n_labels", "n_maps", "n_layers", "use_dilation", "pool_h", "pool_w", "height", "width")]
+        "n_labels", "n_maps", "n_layers", "use_dilation", "pool_h", "pool_w", "height", "width", "precision")]
+
+
+PRECISIONS = {"f32": 0, "bf16": 1}
 
 
 class CnnDesc(ctypes.Structure):

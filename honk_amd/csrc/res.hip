@@ -329,8 +329,15 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
 // --------------------------------------------------------------------------- //
 // conv0: 1 -> C, 3x3, pad 1, ReLU, optional avg-pool (PH x PW); NHWC(CP) out
 // --------------------------------------------------------------------------- //
-template <int PH, int PW>
-__global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ out,
+__device__ __forceinline__ void store4(float* o, f32x4 v) { *(f32x4*)o = v; }
+__device__ __forceinline__ void store4(__bf16* o, f32x4 v) {
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  const b4 b = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  *(b4*)o = b;
+}
+
+template <int PH, int PW, typename OT>
+__global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, OT* __restrict__ out,
                                                     const float* __restrict__ w0, int n, int Hin,
                                                     int Win, int H, int W, int C, int CP) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -352,7 +359,7 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
       win[r][c] = (ir >= 0 && ir < Hin && ic >= 0 && ic < Win) ? xb[(int64_t)ir * Win + ic] : 0.f;
     }
   }
-  float* o = out + gid * CP;
+  OT* o = out + gid * CP;
   const float inv = 1.0f / (float)(PH * PW);
   for (int c4 = 0; c4 < CP; c4 += 4) {
     float v[4];
@@ -380,13 +387,14 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
       }
       v[u] = s;
     }
-    *(f32x4*)(o + c4) = f32x4{v[0], v[1], v[2], v[3]};
+    store4(o + c4, f32x4{v[0], v[1], v[2], v[3]});
   }
 }
 
 // generic pool shape (any PH, PW): same math, input read through L1
+template <typename OT>
 __global__ __launch_bounds__(256) void conv0_generic_kernel(const float* __restrict__ x,
-                                                            float* __restrict__ out,
+                                                            OT* __restrict__ out,
                                                             const float* __restrict__ w0, int n,
                                                             int Hin, int Win, int H, int W, int C,
                                                             int CP, int PH, int PW) {
@@ -398,7 +406,7 @@ __global__ __launch_bounds__(256) void conv0_generic_kernel(const float* __restr
   const int oh = (int)(t % H);
   const int b = (int)(t / H);
   const float* xb = x + (int64_t)b * Hin * Win;
-  float* o = out + gid * CP;
+  OT* o = out + gid * CP;
   const float inv = 1.0f / (float)(PH * PW);
   for (int c = 0; c < CP; ++c) {
     float s = 0.f;
@@ -416,7 +424,7 @@ __global__ __launch_bounds__(256) void conv0_generic_kernel(const float* __restr
         }
       if (PH * PW > 1) s *= inv;
     }
-    o[c] = s;
+    o[c] = (OT)s;
   }
 }
 
@@ -474,6 +482,8 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
   }
 }
 
+#include "res_bf16.inc"
+
 // --------------------------------------------------------------------------- //
 // weight packing
 // --------------------------------------------------------------------------- //
@@ -525,9 +535,10 @@ __global__ void copy_kernel(const float* __restrict__ src, float* __restrict__ d
 // host side
 // --------------------------------------------------------------------------- //
 struct Layout {
-  int C, CP, NT, L, NL;
+  int C, CP, NT, L, NL, prec, KS16;
   int Hin, Win, H, W, ph, pw;
-  size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, total;
+  size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, off_frag16, frag16_floats,
+      total;
 };
 
 static size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
@@ -559,7 +570,14 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   L->off_wout = L->off_bn + round64((size_t)2 * L->CP * L->L);
   L->off_bout = L->off_wout + round64((size_t)L->NL * L->C);
   L->off_zeros = L->off_bout + round64((size_t)L->NL);
-  L->total = L->off_zeros + 64;
+  // bf16 B fragments [L][3][KS][NT][64][8] (bf16) for the HONK_PREC_BF16 kernel
+  L->KS16 = (6 * L->NT + 3) / 4;
+  L->off_frag16 = L->off_zeros + 64;
+  L->frag16_floats = (size_t)3 * L->KS16 * L->NT * 64 * 8 / 2;
+  L->total = L->off_frag16 + L->frag16_floats * L->L;
+  L->prec = d->precision;
+  if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16)
+    return fail(HONK_ERR_ARG, "unknown precision %d", d->precision);
   return HONK_OK;
 }
 
@@ -600,6 +618,49 @@ static Plan plan_block(const Layout& L) {
   return best;
 }
 
+// bf16 kernel plan: 8 waves x MT m-tiles (MT*NT even for a uniform DMA count)
+static Plan plan_block16(const Layout& L) {
+  Plan best{L.NT, 0, 1, L.H};
+  double best_cost = 1e30;
+  const int mts[2] = {4, 2};
+  for (int mi = 0; mi < 2; ++mi) {
+    const int MT = mts[mi];
+    if ((MT * L.NT) % 2) continue;
+    const int MP = 128 * MT;
+    const int thmax = MP / L.W;
+    if (thmax < 1) continue;
+    const int nb = (L.H + thmax - 1) / thmax;
+    const int th = (L.H + nb - 1) / nb;
+    const double cost = (double)nb * MP * (1.0 + 1.0 / MT);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = Plan{L.NT, MT, th, nb};
+    }
+  }
+  return best;
+}
+
+template <int NT, int MT>
+static int launch_block16(const Block16Args& a, hipStream_t st) {
+  using G = G16<NT, MT>;
+  int grid = cu_count();
+  if (grid > a.ntiles) grid = a.ntiles;
+  if (a.chsum)
+    hipLaunchKernelGGL((block16_kernel<NT, MT, true>), dim3(grid), dim3(G::NTHREADS), 0, st, a);
+  else
+    hipLaunchKernelGGL((block16_kernel<NT, MT, false>), dim3(grid), dim3(G::NTHREADS), 0, st, a);
+  HONK_LAUNCH_CHECK("res block16_kernel");
+  return HONK_OK;
+}
+
+static int dispatch_block16(const Plan& p, const Block16Args& a, hipStream_t st) {
+#define HONK_CASE16(nt, mt) \
+  if (p.NT == nt && p.MT == mt) return launch_block16<nt, mt>(a, st);
+  HONK_CASE16(1, 2) HONK_CASE16(1, 4) HONK_CASE16(2, 2) HONK_CASE16(2, 4) HONK_CASE16(3, 2) HONK_CASE16(3, 4)
+#undef HONK_CASE16
+  return fail(HONK_ERR_UNSUPPORTED, "no bf16 block kernel for NT=%d MT=%d", p.NT, p.MT);
+}
+
 template <int NT, int MT>
 static int launch_block(const BlockArgs& a, hipStream_t st) {
   using G = Geo<NT, MT>;
@@ -623,22 +684,68 @@ static int dispatch_block(const Plan& p, const BlockArgs& a, hipStream_t st) {
   return fail(HONK_ERR_UNSUPPORTED, "no block kernel for NT=%d MT=%d", p.NT, p.MT);
 }
 
-static int launch_conv0(const Layout& L, const float* x, float* out, const float* w0, int64_t n,
+template <typename OT>
+static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w0, int64_t n,
                         hipStream_t st) {
   const int64_t total = n * L.H * L.W;
   const int blocks = (int)cdiv(total, 256);
 #define HONK_C0(PH, PW)                                                                        \
   if (L.ph == PH && L.pw == PW) {                                                              \
-    hipLaunchKernelGGL((conv0_kernel<PH, PW>), dim3(blocks), dim3(256), 0, st, x, out, w0,     \
+    hipLaunchKernelGGL((conv0_kernel<PH, PW, OT>), dim3(blocks), dim3(256), 0, st, x, out, w0, \
                        (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                             \
     HONK_LAUNCH_CHECK("res conv0_kernel");                                                     \
     return HONK_OK;                                                                            \
   }
   HONK_C0(1, 1) HONK_C0(2, 2) HONK_C0(4, 3)
 #undef HONK_C0
-  hipLaunchKernelGGL(conv0_generic_kernel, dim3(blocks), dim3(256), 0, st, x, out, w0, (int)n, L.Hin,
+  hipLaunchKernelGGL((conv0_generic_kernel<OT>), dim3(blocks), dim3(256), 0, st, x, out, w0, (int)n, L.Hin,
                      L.Win, L.H, L.W, L.C, L.CP, L.ph, L.pw);
   HONK_LAUNCH_CHECK("res conv0_generic_kernel");
+  return HONK_OK;
+}
+
+// bf16 driver: same schedule as the fp32 one (R / X0 / X1 buffers, fused mean)
+static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* packed, const float* x,
+                        float* logits, int64_t batch, int64_t chunk, void* workspace, hipStream_t st) {
+  const size_t act = (size_t)chunk * L.H * L.W * L.CP;
+  __bf16* R = (__bf16*)workspace;
+  __bf16* X[2] = {R + act, R + 2 * act};
+  float* chsum = (float*)(R + 3 * act);
+  const Plan p = plan_block16(L);
+  const double layer_flop_per_clip = 2.0 * L.H * L.W * L.C * L.C * 9;
+  int rc;
+  for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
+    const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
+    if ((int64_t)n * p.nbands > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
+    rc = launch_conv0(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+    if (rc) return rc;
+    if (L.L == 0) return fail(HONK_ERR_UNSUPPORTED, "bf16 path needs n_layers >= 1");
+    for (int i = 1; i <= L.L; ++i) {
+      Block16Args a;
+      a.in = (i == 1) ? R : X[i & 1];
+      const bool even = (i % 2) == 0;
+      a.res = even ? R : nullptr;
+      a.out_pre = (even && i != L.L) ? R : nullptr;
+      a.out_bn = X[(i + 1) & 1];
+      a.bfrag = (const uint4*)(packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
+      a.bn_scale = packed + L.off_bn + (size_t)2 * L.CP * (i - 1);
+      a.bn_shift = a.bn_scale + L.CP;
+      a.chsum = (i == L.L) ? chsum : nullptr;
+      a.H = L.H;
+      a.W = L.W;
+      a.dil = d->use_dilation ? (1 << ((i - 1) / 3)) : 1;
+      a.TH = p.TH;
+      a.nbands = p.nbands;
+      a.ntiles = (int)(n * p.nbands);
+      TimedLaunch tl(st, layer_flop_per_clip * (double)n);
+      rc = dispatch_block16(p, a, st);
+      tl.done(st);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+                       packed + L.off_bout, logits + c0 * L.NL, p.nbands * 8, L.H * L.W, L.C, L.CP, L.NL);
+    HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16)");
+  }
   return HONK_OK;
 }
 
@@ -660,6 +767,10 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   Layout L;
   if (make_layout(d, &L) != HONK_OK || batch < 1) return 0;
   const int64_t ch = chunk_clips(L, batch);
+  if (L.prec == HONK_PREC_BF16) {
+    const Plan p = plan_block16(L);
+    return (size_t)3 * ch * L.H * L.W * L.CP * 2 + (size_t)ch * p.nbands * 8 * L.CP * sizeof(float);
+  }
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
 }
@@ -684,6 +795,10 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
                        packed + L.off_layers + (size_t)i * L.layer_floats, L.C, L.NT);
     HONK_LAUNCH_CHECK("pack_block");
     float* sc = packed + L.off_bn + (size_t)2 * L.CP * i;
+    const int n16 = 3 * L.KS16 * L.NT * 64 * 8;
+    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i],
+                       (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16);
+    HONK_LAUNCH_CHECK("pack_block16");
     hipLaunchKernelGGL(pack_bn_kernel, dim3(1), dim3(64), 0, st, t[1 + L.L + 2 * i],
                        t[1 + L.L + 2 * i + 1], sc, sc + L.CP, L.C, L.CP);
     HONK_LAUNCH_CHECK("pack_bn");
@@ -712,6 +827,7 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
     return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
   hipStream_t st = (hipStream_t)stream;
   const int64_t chunk = chunk_clips(L, batch);
+  if (L.prec == HONK_PREC_BF16) return forward_bf16(L, d, packed, x, logits, batch, chunk, workspace, st);
   const size_t act = (size_t)chunk * L.H * L.W * L.CP;
   float* R = (float*)workspace;
   float* X[2] = {R + act, R + 2 * act};

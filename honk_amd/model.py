@@ -144,6 +144,9 @@ class SpeechResModel(SerializableModule):
                                pool_w=int(pool[1]) if pool is not None else 0)
         self._honk_packed = None
         self._honk_key = None
+        # "f32": exact fp32 path (1e-4 logit parity); "bf16": bf16 activations/weights
+        # with fp32 accumulation (configs C3/C4; parity = top-1 agreement)
+        self.honk_precision = "f32"
 
     # -- reference forward (CPU tensors / training mode): model.py:104-121 --
     def _torch_forward(self, x):
@@ -177,8 +180,10 @@ class SpeechResModel(SerializableModule):
         return ts
 
     def _desc(self, height, width):
-        d = _native.ResDesc(height=height, width=width, **self._honk_desc)
-        return d
+        if self.honk_precision not in _native.PRECISIONS:
+            raise ValueError(f"honk_precision must be one of {sorted(_native.PRECISIONS)}")
+        return _native.ResDesc(height=height, width=width, precision=_native.PRECISIONS[self.honk_precision],
+                               **self._honk_desc)
 
     def _packed(self, x):
         lib = _native.load()
