@@ -87,28 +87,40 @@ __device__ __forceinline__ void wait_vmcnt() {
 // buffer bounds check returns zeros (= the reference's zero padding).
 template <int NT, int MT>
 __device__ __forceinline__ void issue_stage(const BlockArgs& a, int tile, int dy, float* buf, int wave,
-                                            int lane) {
+                                            const unsigned (&gpack)[MT]) {
   using G = Geo<NT, MT>;
   const int b = tile / a.nbands;
   const int h0 = (tile - b * a.nbands) * a.TH;
   const int clip_floats = a.H * a.W * G::CP;
   __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.in + (size_t)b * clip_floats), (short)0, clip_floats * 4, 0x00020000);
-  const int total = a.TH * a.W * G::CH4;
-  const int rshift = (dy - 1) * a.dil;
+  const int rbase = h0 + (dy - 1) * a.dil;   // wave-uniform
+  const unsigned row_bytes = (unsigned)(a.W * G::CP * 4);
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int pc = wave + i * G::NWAVES;
-    const int ci = (pc << 6) + lane;
+    // gpack: (band row << 16) | byte offset within the row; row 0xffff = past the band
+    const int grow = rbase + (int)(gpack[i] >> 16);
+    const unsigned voff = ((unsigned)grow < (unsigned)a.H) ? (unsigned)grow * row_bytes + (gpack[i] & 0xffffu)
+                                                           : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(buf + (pc << 8)),
+                                             16, voff, 0, 0, 0);
+  }
+}
+
+// per-lane, tile-invariant part of the staging addresses (see issue_stage)
+template <int NT, int MT>
+__device__ __forceinline__ void make_gpack(const BlockArgs& a, int wave, int lane, unsigned (&gpack)[MT]) {
+  using G = Geo<NT, MT>;
+  const int total = a.TH * a.W * G::CH4;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int ci = ((wave + i * G::NWAVES) << 6) + lane;
     const int pix = ci / G::CH4;
     const int ch = ci - pix * G::CH4;
     const int r = pix / a.W;
     const int w = pix - r * a.W;
-    const int grow = h0 + r + rshift;
-    const bool ok = (ci < total) && (grow >= 0) && (grow < a.H);
-    const unsigned voff = ok ? (unsigned)(((grow * a.W + w) * G::CP + ch * 4) * 4) : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(buf + (pc << 8)),
-                                             16, voff, 0, 0, 0);
+    gpack[i] = (ci < total) ? ((unsigned)r << 16) | (unsigned)((w * G::CP + ch * 4) * 4) : 0xffff0000u;
   }
 }
 
@@ -125,10 +137,10 @@ __device__ __forceinline__ void load_b_dx(__amdgpu_buffer_rsrc_t wr, int dy, int
 // MFMAs of step K run; after the last q of a dx, that dx's B registers are
 // refilled with the next stage's fragments (row offset NDY) so the L2 latency
 // hides under the remaining MFMAs.  Template recursion keeps register indices static.
-template <int NT, int MT, int NDY, int K>
+template <int NT, int MT, int NDY, int K, typename Mid>
 __device__ __forceinline__ void stage_step(const char* base, const int (&aoff)[3][MT], f32x4 (&bcur)[3][NT],
                                            f32x4 (&acc)[MT], f32x4 (&a0)[MT], f32x4 (&a1)[MT],
-                                           __amdgpu_buffer_rsrc_t wr, int lane16) {
+                                           __amdgpu_buffer_rsrc_t wr, int lane16, Mid& mid) {
   constexpr int NK = 3 * NT;
   if constexpr (K < NK) {
     constexpr int dx = K / NT, q = K % NT;
@@ -145,20 +157,24 @@ __device__ __forceinline__ void stage_step(const char* base, const int (&aoff)[3
       for (int m = 0; m < MT; ++m)
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[m][j], bcur[dx][q][j], acc[m], 0, 0, 0);
     }
+    // after the first step's MFMAs are issued: next-stage LDS-DMA (+ residual
+    // prefetch), whose VALU address math then overlaps the other waves' MFMAs.
+    // It precedes every B refill, so the barrier's vmcnt count stays exact.
+    if constexpr (K == 0) mid();
     if constexpr (q == NT - 1) load_b_dx<NT>(wr, NDY, dx, lane16, bcur[dx]);
     __builtin_amdgcn_sched_barrier(0);
-    stage_step<NT, MT, NDY, K + 1>(base, aoff, bcur, acc, a0, a1, wr, lane16);
+    stage_step<NT, MT, NDY, K + 1>(base, aoff, bcur, acc, a0, a1, wr, lane16, mid);
   }
 }
 
-template <int NT, int MT, int NDY>
+template <int NT, int MT, int NDY, typename Mid>
 __device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff)[3][MT], f32x4 (&bcur)[3][NT],
-                                              f32x4 (&acc)[MT], __amdgpu_buffer_rsrc_t wr, int lane16) {
+                                              f32x4 (&acc)[MT], __amdgpu_buffer_rsrc_t wr, int lane16, Mid& mid) {
   const char* base = (const char*)cur;
   f32x4 a0[MT], a1[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) a0[m] = *(const f32x4*)(base + aoff[0][m]);
-  stage_step<NT, MT, NDY, 0>(base, aoff, bcur, acc, a0, a1, wr, lane16);
+  stage_step<NT, MT, NDY, 0>(base, aoff, bcur, acc, a0, a1, wr, lane16, mid);
 }
 
 template <int NT, int MT, bool LAST>
@@ -234,7 +250,9 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   };
 
   // prologue: stage (tile, dy=0) and its B fragments, fully landed before the loop
-  issue_stage<NT, MT>(a, tile, 0, smem, wave, lane);
+  unsigned gpack[MT];
+  make_gpack<NT, MT>(a, wave, lane, gpack);
+  issue_stage<NT, MT>(a, tile, 0, smem, wave, gpack);
 #pragma unroll
   for (int dx = 0; dx < 3; ++dx) load_b_dx<NT>(wr, 0, dx, lane16, bcur[dx]);
   wait_vmcnt<0>();
@@ -255,17 +273,19 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
     float* nxt = smem + ((s + 1) & 1) * G::BUF;                                         \
     if (DY == 0) wait_vmcnt<G::VM_AFTER_GLDS_LAST>(); else wait_vmcnt<G::VM_AFTER_GLDS>(); \
     __builtin_amdgcn_s_barrier();                                                       \
-    if (DY < 2)                                                                         \
-      issue_stage<NT, MT>(a, tile, DY + 1, nxt, wave, lane);                            \
-    else if (tile + GR < a.ntiles)                                                      \
-      issue_stage<NT, MT>(a, tile + GR, 0, nxt, wave, lane);                            \
-    if (DY == 2 && !LAST) {                                                             \
-      const __amdgpu_buffer_rsrc_t rr = tile_rsrc(a.res);                               \
-      _Pragma("unroll") for (int m = 0; m < MT; ++m)                                    \
-        rv[m] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(        \
-            rr, eoff, m * 16 * G::CP * 4, 0));                                          \
-    }                                                                                   \
-    compute_stage<NT, MT, (DY + 1) % 3>(cur, aoff, bcur, acc, wr, lane16);              \
+    auto mid = [&]() {                                                                  \
+      if (DY < 2)                                                                       \
+        issue_stage<NT, MT>(a, tile, DY + 1, nxt, wave, gpack);                         \
+      else if (tile + GR < a.ntiles)                                                    \
+        issue_stage<NT, MT>(a, tile + GR, 0, nxt, wave, gpack);                         \
+      if (DY == 2 && !LAST) {                                                           \
+        const __amdgpu_buffer_rsrc_t rr = tile_rsrc(a.res);                             \
+        _Pragma("unroll") for (int m = 0; m < MT; ++m)                                  \
+          rv[m] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(      \
+              rr, eoff, m * 16 * G::CP * 4, 0));                                        \
+      }                                                                                 \
+    };                                                                                  \
+    compute_stage<NT, MT, (DY + 1) % 3>(cur, aoff, bcur, acc, wr, lane16, mid);         \
     ++s;                                                                                \
   }
     HONK_STAGE(0)
@@ -563,6 +583,8 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   L->H = L->Hin / L->ph;
   L->W = L->Win / L->pw;
   if (L->H < 1 || L->W < 1) return fail(HONK_ERR_ARG, "pool larger than input");
+  if (L->W * L->CP * 4 > 65535)  // staging offsets pack the row byte offset in 16 bits
+    return fail(HONK_ERR_UNSUPPORTED, "feature-map width %d too large for the staging plan", L->W);
   L->off_conv0 = 0;
   L->off_layers = round64((size_t)L->CP * 9);
   L->layer_floats = (size_t)9 * L->CP * L->CP;
