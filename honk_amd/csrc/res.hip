@@ -51,8 +51,7 @@ struct Geo {
   static constexpr int MP = 16 * MT * MW;     // max pixels per tile
   static constexpr int ZOFF = MP * CP;        // zero pixel (floats); MP*CP*4 = MT*NWAVES KiB
   static constexpr int BUF = ZOFF + CP;       // floats per LDS stage buffer
-  static constexpr int SCR = 2 * BUF;         // per-wave 16x16 epilogue transpose scratch
-  static constexpr int LDS_FLOATS = SCR + NWAVES * 256;
+  static constexpr int LDS_FLOATS = 2 * BUF;
   // VMEM ops a wave issues per stage after its glds: B refills (3*NT) and, in
   // the tile's last stage, residual loads (MT) + pre/BN stores (2*MT)
   static constexpr int VM_AFTER_GLDS = 3 * NT;
@@ -155,7 +154,9 @@ __device__ __forceinline__ void stage_step(const char* base, const int (&aoff)[3
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
       for (int m = 0; m < MT; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[m][j], bcur[dx][q][j], acc[m], 0, 0, 0);
+        // weights as the A operand, activations as B: D = W . X^T, so the C/D layout
+        // gives each lane 4 consecutive out-channels (rows 4g+r) of pixel i16
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(bcur[dx][q][j], cur[m][j], acc[m], 0, 0, 0);
     }
     // after the first step's MFMAs are issued: next-stage LDS-DMA (+ residual
     // prefetch), whose VALU address math then overlaps the other waves' MFMAs.
@@ -181,7 +182,7 @@ template <int NT, int MT, bool LAST>
 __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(BlockArgs a) {
   using G = Geo<NT, MT>;
   // ONE LDS array (a second __shared__ object can de-pipeline glds waits):
-  // [stage buffer 0 | stage buffer 1 | per-wave transpose scratch]
+  // [stage buffer 0 | stage buffer 1]
   __shared__ __attribute__((aligned(16))) float smem[G::LDS_FLOATS];
 
   const int tid = threadIdx.x;
@@ -191,8 +192,6 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   const int mg = wave / NT;
   const int g = lane >> 4;
   const int i16 = lane & 15;
-  const int t4 = (lane >> 2) & 3;  // epilogue: 16-byte channel chunk
-  const int u4 = lane & 3;         // epilogue: pixel row within the 4-row group
 
   for (int t = tid; t < G::CP; t += G::NTHREADS) {
     smem[G::ZOFF + t] = 0.f;
@@ -223,13 +222,12 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
     }
   }
 
-  // epilogue constants: after the 16x16 transpose lane (g, t4, u4) holds pixel
-  // row 4g+u4 of an m-tile, out channels nt*16 + 4*t4 .. +3 (one 16-byte chunk)
-  const int c4 = nt * 16 + 4 * t4;
+  // epilogue constants: lane (g, i16) owns pixel i16 of each m-tile and out
+  // channels nt*16 + 4g .. +3 (one 16-byte chunk)
+  const int c4 = nt * 16 + 4 * g;
   const f32x4 bsc = *(const f32x4*)(a.bn_scale + c4);
   const f32x4 bsh = *(const f32x4*)(a.bn_shift + c4);
-  const int eoff = ((mg * MT * 16 + 4 * g + u4) * G::CP + c4) * 4;
-  float* scr = smem + G::SCR + wave * 256;
+  const int eoff = ((mg * MT * 16 + i16) * G::CP + c4) * 4;
 
   // XCD-aware tile order: blocks sharing an XCD (bid % 8) walk adjacent tiles
   const int GR = gridDim.x;
@@ -293,30 +291,26 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
     HONK_STAGE(2)
 #undef HONK_STAGE
 
-    // epilogue: 16x16 transpose of each accumulator tile through this wave's
-    // LDS scratch (C/D layout: lane holds rows g*4+r, column i16), then ReLU,
-    // residual add, pre-BN store (even layers) and BN store, 16 B per lane.
-    // Stores past the tile's valid pixels are dropped by the bounds check.  In
-    // the last layer (chsum != nullptr) nothing is stored: the BN output is
-    // summed per channel over the tile's valid pixels instead (fused mean).
+    // epilogue: lane (g, i16) holds out channels c4..c4+3 of pixel i16 of each
+    // m-tile: ReLU, residual add, pre-BN store (even layers) and BN store, 16 B
+    // per lane; stores past the tile's valid pixels are dropped by the bounds
+    // check.  In the last layer nothing is stored: the BN output is summed per
+    // channel over the tile's valid pixels instead (fused spatial mean).
     {
       const __amdgpu_buffer_rsrc_t bn_r = tile_rsrc(LAST ? nullptr : a.out_bn);
       const __amdgpu_buffer_rsrc_t pre_r = tile_rsrc(a.out_pre);
       const int b = tile / a.nbands;
-      const int lim = min(a.TH, a.H - (tile - b * a.nbands) * a.TH) * a.W - (mg * MT * 16 + 4 * g + u4);
+      const int lim = min(a.TH, a.H - (tile - b * a.nbands) * a.TH) * a.W - (mg * MT * 16 + i16);
       f32x4 csum = {0.f, 0.f, 0.f, 0.f};
       const __amdgpu_buffer_rsrc_t rr = tile_rsrc(a.res);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         if (LAST)  // last layer: residual loaded here (no prefetch registers)
           rv[m] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, eoff, m * 16 * G::CP * 4, 0));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) scr[(4 * g + r) * 16 + i16] = acc[m][r];
-        const f32x4 d = *(const f32x4*)(scr + (4 * g + u4) * 16 + 4 * t4);
         f32x4 v, o;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          v[k] = fmaxf(d[k], 0.f) + rv[m][k];
+          v[k] = fmaxf(acc[m][k], 0.f) + rv[m][k];
           o[k] = fmaf(v[k], bsc[k], bsh[k]);
         }
         const int so = m * 16 * G::CP * 4;
@@ -327,18 +321,17 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
         if (LAST && m * 16 < lim) csum += o;
       }
       if (LAST) {
-        // reduce over the 16 lanes holding the same 4 channels (u4: xor 1,2; g: xor 16,32)
+        // reduce over the 16 lanes (pixels) holding the same 4 channels
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float t = csum[k];
           t += __shfl_xor(t, 1);
           t += __shfl_xor(t, 2);
-          t += __shfl_xor(t, 16);
-          t += __shfl_xor(t, 32);
+          t += __shfl_xor(t, 4);
+          t += __shfl_xor(t, 8);
           csum[k] = t;
         }
-        if ((lane & 0x33) == 0)
-          *(f32x4*)(a.chsum + ((size_t)tile * MW + mg) * G::CP + c4) = csum;
+        if (i16 == 0) *(f32x4*)(a.chsum + ((size_t)tile * MW + mg) * G::CP + c4) = csum;
       }
     }
     tile += GR;
