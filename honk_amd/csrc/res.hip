@@ -475,9 +475,13 @@ __global__ __launch_bounds__(256) void tail_kernel(const float* __restrict__ x, 
 }
 
 // logits[b] = Wout . (sum of the fused per-tile channel sums) / HW + bout
+// bn_scale/bn_shift: the last layer's BatchNorm applied to the channel means
+// (bf16 path, whose activations are pre-BN), or nullptr (fp32 path)
 __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ chsum, const float* __restrict__ wout,
                                                       const float* __restrict__ bout, float* __restrict__ logits,
-                                                      int nparts, int HW, int C, int CP, int NL) {
+                                                      int nparts, int HW, int C, int CP, int NL,
+                                                      const float* __restrict__ bn_scale,
+                                                      const float* __restrict__ bn_shift) {
   __shared__ float mean[64];
   const int b = blockIdx.x;
   const int c = threadIdx.x;
@@ -485,7 +489,7 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
     const float* p = chsum + (size_t)b * nparts * CP + c;
     float s = 0.f;
     for (int i = 0; i < nparts; ++i) s += p[(size_t)i * CP];
-    mean[c] = s / (float)HW;
+    mean[c] = bn_scale ? fmaf(s / (float)HW, bn_scale[c], bn_shift[c]) : s / (float)HW;
   }
   __syncthreads();
   for (int n = c; n < NL; n += blockDim.x) {
@@ -551,7 +555,7 @@ struct Layout {
   int C, CP, NT, L, NL, prec, KS16;
   int Hin, Win, H, W, ph, pw;
   size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, off_frag16, frag16_floats,
-      total;
+      off_bias16, total;
 };
 
 static size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
@@ -589,7 +593,9 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   L->KS16 = (6 * L->NT + 3) / 4;
   L->off_frag16 = L->off_zeros + 64;
   L->frag16_floats = (size_t)3 * L->KS16 * L->NT * 64 * 8 / 2;
-  L->total = L->off_frag16 + L->frag16_floats * L->L;
+  // folded input-BN bias [L][16 classes][CP] for the bf16 kernel
+  L->off_bias16 = L->off_frag16 + L->frag16_floats * L->L;
+  L->total = L->off_bias16 + (size_t)16 * L->CP * L->L;
   L->prec = d->precision;
   if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16)
     return fail(HONK_ERR_ARG, "unknown precision %d", d->precision);
@@ -633,46 +639,36 @@ static Plan plan_block(const Layout& L) {
   return best;
 }
 
-// bf16 kernel plan: 8 waves x MT m-tiles (MT*NT even for a uniform DMA count)
+// bf16 kernel plan: 8 waves x MT m-tiles; MT is the largest whose 3-buffer ring
+// plus the layer's weights fit the 160 KiB LDS (NT = 3 -> 3, else 4)
 static Plan plan_block16(const Layout& L) {
-  Plan best{L.NT, 0, 1, L.H};
-  double best_cost = 1e30;
-  const int mts[2] = {4, 2};
-  for (int mi = 0; mi < 2; ++mi) {
-    const int MT = mts[mi];
-    if ((MT * L.NT) % 2) continue;
-    const int MP = 128 * MT;
-    const int thmax = MP / L.W;
-    if (thmax < 1) continue;
-    const int nb = (L.H + thmax - 1) / thmax;
-    const int th = (L.H + nb - 1) / nb;
-    const double cost = (double)nb * MP * (1.0 + 1.0 / MT);
-    if (cost < best_cost - 1e-9) {
-      best_cost = cost;
-      best = Plan{L.NT, MT, th, nb};
-    }
-  }
-  return best;
+  const int MT = (L.NT == 3) ? 3 : 4;
+  const int MP = 128 * MT;
+  const int thmax = MP / L.W;  // >= 1: make_layout bounds W
+  const int nb = (L.H + thmax - 1) / thmax;
+  const int th = (L.H + nb - 1) / nb;
+  return Plan{L.NT, MT, th, nb};
 }
 
 template <int NT, int MT>
 static int launch_block16(const Block16Args& a, hipStream_t st) {
   using G = G16<NT, MT>;
+  static_assert(G::LDS <= 160 * 1024, "LDS");
   int grid = cu_count();
   if (grid > a.ntiles) grid = a.ntiles;
-  if (a.chsum)
-    hipLaunchKernelGGL((block16_kernel<NT, MT, true>), dim3(grid), dim3(G::NTHREADS), 0, st, a);
-  else
-    hipLaunchKernelGGL((block16_kernel<NT, MT, false>), dim3(grid), dim3(G::NTHREADS), 0, st, a);
+  const dim3 gd(grid), bd(G::NTHREADS);
+  if (a.chsum && a.res) hipLaunchKernelGGL((block16_kernel<NT, MT, true, true>), gd, bd, 0, st, a);
+  else if (a.chsum) hipLaunchKernelGGL((block16_kernel<NT, MT, true, false>), gd, bd, 0, st, a);
+  else if (a.res) hipLaunchKernelGGL((block16_kernel<NT, MT, false, true>), gd, bd, 0, st, a);
+  else hipLaunchKernelGGL((block16_kernel<NT, MT, false, false>), gd, bd, 0, st, a);
   HONK_LAUNCH_CHECK("res block16_kernel");
   return HONK_OK;
 }
 
 static int dispatch_block16(const Plan& p, const Block16Args& a, hipStream_t st) {
-#define HONK_CASE16(nt, mt) \
-  if (p.NT == nt && p.MT == mt) return launch_block16<nt, mt>(a, st);
-  HONK_CASE16(1, 2) HONK_CASE16(1, 4) HONK_CASE16(2, 2) HONK_CASE16(2, 4) HONK_CASE16(3, 2) HONK_CASE16(3, 4)
-#undef HONK_CASE16
+  if (p.NT == 1 && p.MT == 4) return launch_block16<1, 4>(a, st);
+  if (p.NT == 2 && p.MT == 4) return launch_block16<2, 4>(a, st);
+  if (p.NT == 3 && p.MT == 3) return launch_block16<3, 3>(a, st);
   return fail(HONK_ERR_UNSUPPORTED, "no bf16 block kernel for NT=%d MT=%d", p.NT, p.MT);
 }
 
@@ -720,31 +716,32 @@ static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w
 }
 
 // bf16 driver: same schedule as the fp32 one (R / X0 / X1 buffers, fused mean)
+// bf16 schedule: activations stay pre-BN (see res_bf16.inc), so one residual
+// stream R (conv0 output, then every even layer's sum, in place) and one odd-layer
+// buffer X suffice; each layer writes exactly one tensor.
 static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* packed, const float* x,
                         float* logits, int64_t batch, int64_t chunk, void* workspace, hipStream_t st) {
   const size_t act = (size_t)chunk * L.H * L.W * L.CP;
   __bf16* R = (__bf16*)workspace;
-  __bf16* X[2] = {R + act, R + 2 * act};
-  float* chsum = (float*)(R + 3 * act);
+  __bf16* X = R + act;
+  float* chsum = (float*)(R + 2 * act);
   const Plan p = plan_block16(L);
   const double layer_flop_per_clip = 2.0 * L.H * L.W * L.C * L.C * 9;
+  if (L.L == 0) return fail(HONK_ERR_UNSUPPORTED, "bf16 path needs n_layers >= 1");
   int rc;
   for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
     const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
     if ((int64_t)n * p.nbands > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
     rc = launch_conv0(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
     if (rc) return rc;
-    if (L.L == 0) return fail(HONK_ERR_UNSUPPORTED, "bf16 path needs n_layers >= 1");
     for (int i = 1; i <= L.L; ++i) {
-      Block16Args a;
-      a.in = (i == 1) ? R : X[i & 1];
       const bool even = (i % 2) == 0;
+      Block16Args a;
+      a.in = even ? X : R;
       a.res = even ? R : nullptr;
-      a.out_pre = (even && i != L.L) ? R : nullptr;
-      a.out_bn = X[(i + 1) & 1];
+      a.out = (i == L.L) ? nullptr : (even ? R : X);
       a.bfrag = (const uint4*)(packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
-      a.bn_scale = packed + L.off_bn + (size_t)2 * L.CP * (i - 1);
-      a.bn_shift = a.bn_scale + L.CP;
+      a.bias = packed + L.off_bias16 + (size_t)16 * L.CP * (i - 1);
       a.chsum = (i == L.L) ? chsum : nullptr;
       a.H = L.H;
       a.W = L.W;
@@ -757,8 +754,10 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       tl.done(st);
       if (rc) return rc;
     }
+    const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
     hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
-                       packed + L.off_bout, logits + c0 * L.NL, p.nbands * 8, L.H * L.W, L.C, L.CP, L.NL);
+                       packed + L.off_bout, logits + c0 * L.NL, p.nbands * 8, L.H * L.W, L.C, L.CP, L.NL,
+                       bn_last, bn_last + L.CP);
     HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16)");
   }
   return HONK_OK;
@@ -784,7 +783,7 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   const int64_t ch = chunk_clips(L, batch);
   if (L.prec == HONK_PREC_BF16) {
     const Plan p = plan_block16(L);
-    return (size_t)3 * ch * L.H * L.W * L.CP * 2 + (size_t)ch * p.nbands * 8 * L.CP * sizeof(float);
+    return (size_t)2 * ch * L.H * L.W * L.CP * 2 + (size_t)ch * p.nbands * 8 * L.CP * sizeof(float);
   }
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
@@ -810,10 +809,16 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
                        packed + L.off_layers + (size_t)i * L.layer_floats, L.C, L.NT);
     HONK_LAUNCH_CHECK("pack_block");
     float* sc = packed + L.off_bn + (size_t)2 * L.CP * i;
+    // bf16: the input BatchNorm (layer i-1's; none for layer 1) folded into
+    // the weights and the border-class bias; layer i-1's BN was packed above
+    const float* in_bn = (i > 0) ? packed + L.off_bn + (size_t)2 * L.CP * (i - 1) : nullptr;
     const int n16 = 3 * L.KS16 * L.NT * 64 * 8;
-    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i],
+    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
                        (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16);
     HONK_LAUNCH_CHECK("pack_block16");
+    hipLaunchKernelGGL(pack_bias16_kernel, dim3(cdiv(16 * L.CP, 256)), dim3(256), 0, st, t[1 + i],
+                       in_bn ? in_bn + L.CP : nullptr, packed + L.off_bias16 + (size_t)16 * L.CP * i, L.C, L.CP);
+    HONK_LAUNCH_CHECK("pack_bias16");
     hipLaunchKernelGGL(pack_bn_kernel, dim3(1), dim3(64), 0, st, t[1 + L.L + 2 * i],
                        t[1 + L.L + 2 * i + 1], sc, sc + L.CP, L.C, L.CP);
     HONK_LAUNCH_CHECK("pack_bn");
@@ -885,7 +890,8 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
       HONK_LAUNCH_CHECK("res tail_kernel");
     } else {
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
-                         packed + L.off_bout, logits + c0 * L.NL, p.nbands * MW, L.H * L.W, L.C, L.CP, L.NL);
+                         packed + L.off_bout, logits + c0 * L.NL, p.nbands * MW, L.H * L.W, L.C, L.CP, L.NL,
+                         (const float*)nullptr, (const float*)nullptr);
       HONK_LAUNCH_CHECK("res tail_sum_kernel");
     }
   }
