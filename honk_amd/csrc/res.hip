@@ -753,6 +753,24 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       rc = dispatch_block16(p, a, st);
       tl.done(st);
       if (rc) return rc;
+#ifdef HONK_STAMP
+      {
+        static unsigned long long h[256 * 8 * 8];
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(honk_stamp_buf), sizeof(h));
+        double sum[7] = {0};
+        int nw = 0;
+        for (int w = 0; w < 256 * 8; ++w)
+          if (h[w * 8 + 7]) {
+            for (int q = 0; q < 7; ++q) sum[q] += (double)h[w * 8 + q];
+            ++nw;
+          }
+        if (nw)
+          fprintf(stderr, "stamp layer %d dil %d: w0 %.3f c0 %.3f w1 %.3f c1 %.3f w2 %.3f c2 %.3f (of %.0f)\n", i, a.dil,
+                  sum[0] / sum[6], sum[1] / sum[6], sum[2] / sum[6], sum[3] / sum[6], sum[4] / sum[6],
+                  sum[5] / sum[6], sum[6] / nw);
+      }
+#endif
     }
     const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
     hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,

@@ -68,6 +68,26 @@ def test_bf16_overrides(override):
     assert np.mean(out.argmax(1) == ref.argmax(1)) >= MIN_TOP1
 
 
+def test_bf16_mfcc_like_inputs():
+    """SURVEY §8(d) parity set: per-coefficient MFCC scales (c0 ~ N(-30, 20^2),
+    c_k ~ N(0, (8/(1+k))^2)) exercise the bf16 range of the folded-BN layers."""
+    cfg, params, _, m = _case("res15", 32, seed=11)
+    rng = np.random.Generator(np.random.PCG64(12))
+    scale = np.array([20.0] + [8.0 / (1 + k) for k in range(1, 40)], dtype=np.float32)
+    x = (rng.standard_normal((32, 101, 40)).astype(np.float32) * scale).astype(np.float32)
+    x[:, :, 0] -= 30.0
+    params = orc.calibrate_bn(params, cfg, x[:2], seed=11)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    m = m.to(DEV)
+    out = _run(m, x)
+    ref = orc.forward(params, cfg, x)
+    scale_ref = np.abs(ref).max()
+    err = np.abs(out - ref).max()
+    print(f"mfcc-like: bf16 max|err|={err:.3e} (logit scale {scale_ref:.3f})")
+    assert err <= MAX_ABS * max(1.0, scale_ref)
+    assert np.mean(out.argmax(1) == ref.argmax(1)) >= MIN_TOP1
+
+
 def test_bf16_batch_invariance(monkeypatch):
     cfg, params, x, m = _case("res15", 13, seed=5)
     full = _run(m, x)
