@@ -252,8 +252,90 @@ static int conv(const float* in, const float* w, const float* bias, float* out, 
   return launch_gemm(a, pool2, st);
 }
 
+// Linear with few outputs (n <= NB, e.g. cnn-trad-pool2's 26624 -> 4 output
+// layer): a GEMV per clip, HBM-bound on x.  One 256-thread block per CPB clips
+// walks K with 16-byte loads, every W element read once per block (L2-resident)
+// and reused for the CPB clips; wave shuffles + LDS finish the reduction.  The
+// GEMM kernel would give such a layer only ceil(m / 128) blocks with the whole
+// K serial in each.
+template <int NB, int CPB>
+__global__ __launch_bounds__(256) void linear_small_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ b, float* __restrict__ y,
+                                                           int64_t m, int K, int N, int relu) {
+  __shared__ float red[4][CPB][NB];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * CPB;
+  float acc[CPB][NB];
+#pragma unroll
+  for (int c = 0; c < CPB; ++c)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[c][n] = 0.f;
+  const bool vec = (K & 3) == 0;
+  if (vec) {
+    const int K4 = K >> 2;
+    for (int k4 = tid; k4 < K4; k4 += 256) {
+      float4 xv[CPB];
+#pragma unroll
+      for (int c = 0; c < CPB; ++c)
+        xv[c] = (r0 + c < m) ? ((const float4*)(x + (r0 + c) * K))[k4] : float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        if (n < N) {
+          const float4 wv = ((const float4*)(w + (int64_t)n * K))[k4];
+#pragma unroll
+          for (int c = 0; c < CPB; ++c)
+            acc[c][n] = fmaf(wv.x, xv[c].x, fmaf(wv.y, xv[c].y, fmaf(wv.z, xv[c].z, fmaf(wv.w, xv[c].w, acc[c][n]))));
+        }
+      }
+    }
+  } else {
+    for (int k = tid; k < K; k += 256) {
+      float xv[CPB];
+#pragma unroll
+      for (int c = 0; c < CPB; ++c) xv[c] = (r0 + c < m) ? x[(r0 + c) * K + k] : 0.f;
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+        if (n < N) {
+          const float wv = w[(int64_t)n * K + k];
+#pragma unroll
+          for (int c = 0; c < CPB; ++c) acc[c][n] = fmaf(wv, xv[c], acc[c][n]);
+        }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CPB; ++c)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      float t = acc[c][n];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+      if ((tid & 63) == 0) red[tid >> 6][c][n] = t;
+    }
+  __syncthreads();
+  if (tid < CPB * NB) {
+    const int c = tid / NB, n = tid - c * NB;
+    if (n < N && r0 + c < m) {
+      float v = red[0][c][n] + red[1][c][n] + red[2][c][n] + red[3][c][n] + (b ? b[n] : 0.f);
+      if (relu) v = fmaxf(v, 0.f);
+      y[(r0 + c) * N + n] = v;
+    }
+  }
+}
+
 static int linear(const float* x, const float* w, const float* b, float* y, int64_t m, int k, int n,
                   int relu, hipStream_t st) {
+  if (n <= 16 && m > 0) {
+    constexpr int CPB = 4;
+    const unsigned blocks = (unsigned)cdiv(m, CPB);
+    if (n <= 4)
+      hipLaunchKernelGGL((linear_small_kernel<4, CPB>), dim3(blocks), dim3(256), 0, st, x, w, b, y, m, k, n, relu);
+    else if (n <= 8)
+      hipLaunchKernelGGL((linear_small_kernel<8, CPB>), dim3(blocks), dim3(256), 0, st, x, w, b, y, m, k, n, relu);
+    else
+      hipLaunchKernelGGL((linear_small_kernel<16, CPB>), dim3(blocks), dim3(256), 0, st, x, w, b, y, m, k, n, relu);
+    HONK_LAUNCH_CHECK("linear_small_kernel");
+    return HONK_OK;
+  }
   return conv(x, w, b, y, m, k, 1, 1, n, 1, 1, 1, 1, relu, st);
 }
 
@@ -348,8 +430,9 @@ int honk_maxpool2d_f32(const float* in, float* out, int64_t batch, int32_t c, in
 
 int honk_linear_f32(const float* x, const float* w, const float* b, float* y, int64_t m, int32_t k, int32_t n,
                     int32_t relu, void* stream) {
-  if (!x || !w || !y) return fail(HONK_ERR_ARG, "null pointer argument");
   if (k < 1 || n < 1 || m < 0) return fail(HONK_ERR_ARG, "bad linear shape");
+  if (m == 0) return HONK_OK;
+  if (!x || !w || !y) return fail(HONK_ERR_ARG, "null pointer argument");
   return linear(x, w, b, y, m, k, n, relu, (hipStream_t)stream);
 }
 

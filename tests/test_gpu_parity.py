@@ -180,3 +180,25 @@ def test_conv2d_linear_maxpool_abi():
                                       yl.data_ptr(), 37, 1674, 32, 0, s), "linear")
     torch.cuda.synchronize()
     torch.testing.assert_close(yl.cpu(), torch.nn.functional.linear(xl, wl, bl), atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("m,k,n,relu", [(37, 26624, 4, 0), (9, 1675, 12, 1), (130, 128, 16, 0), (5, 7, 1, 1),
+                                        (0, 64, 4, 0)])
+def test_linear_small_n_abi(m, k, n, relu):
+    """Few-output Linear (cnn-trad-pool2's 26624 -> 4 head): GEMV kernel path,
+    vector (K % 4 == 0) and scalar K loops, ragged clip counts, optional ReLU."""
+    lib = _native.load()
+    g = torch.Generator().manual_seed(m + k + n)
+    x = torch.randn(m, k, generator=g)
+    w = torch.randn(n, k, generator=g) / k ** 0.5
+    b = torch.randn(n, generator=g)
+    y = torch.full((max(m, 1), n), float("nan"), device=DEV)
+    s = _native.stream_handle(torch.device(DEV))
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)  # keep the device copies alive across the launch
+    _native.check(lib.honk_linear_f32(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), y.data_ptr(), m, k, n, relu, s),
+                  "linear")
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.linear(x.double(), w.double(), b.double()).float()
+    if relu:
+        ref = torch.relu(ref)
+    torch.testing.assert_close(y[:m].cpu(), ref, atol=1e-4, rtol=1e-5)
