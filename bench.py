@@ -78,16 +78,21 @@ def cfg_name(cfg):
     return f"res{cfg['n_layers']}-{cfg['n_feature_maps']}maps" if "n_layers" in cfg else "cnn"
 
 
-def load_traffic():
-    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC pass (or None)."""
-    p = os.path.join(REPO, "profiles", "pmc_block_kernel.json")
+def load_traffic(kernel, clips_per_launch):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC pass
+    (profiles/pmc_<kernel>.json, written by tools/pmc_summary.py), or None when no
+    pass was taken for that kernel at this launch size."""
+    p = os.path.join(REPO, "profiles", f"pmc_{kernel}.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            d = json.load(f)
     except Exception:
         return None
+    if d.get("batch_clips_per_launch") != clips_per_launch:
+        return None
+    return d.get("hbm_bytes_per_launch")
 
 
 def train_bench(args, dev, rank, world, barrier):
@@ -173,7 +178,8 @@ def measure_alt_bf16(model, x, args, dev, barrier, hd, _native, orc, cfg, B, wor
             "roofline": {"bound": "mfma", "kernel": "honk::res::block16_kernel (dilated 3x3 conv, bf16 MFMA)",
                          "achieved": round(ach, 2) if ach else None, "peak": BF16_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4) if ach else None,
-                         "avg_launch_ms": round(kms / max(nl, 1), 4)},
+                         "avg_launch_ms": round(kms / max(nl, 1), 4),
+                         "traffic": load_traffic("block16_kernel", min(B, 4096))},
             "parity": {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
                        "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()),
                        "sample_clips": len(idx)},
@@ -293,7 +299,8 @@ def main():
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4) if achieved else None,
-                         "traffic": load_traffic(),
+                         "traffic": (load_traffic("block16_kernel" if bf16 else "block_kernel", min(B, 4096))
+                                     if is_res else None),
                          "launches": nlaunch, "avg_launch_ms": round(avg_ms, 4),
                          "flop_per_launch": kflop / max(nlaunch, 1)},
             "parity": {"top1_agreement_vs_oracle": top1, "max_abs_logit_err_vs_oracle_f64": maxerr,

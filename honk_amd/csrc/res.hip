@@ -349,42 +349,46 @@ __device__ __forceinline__ void store4(__bf16* o, f32x4 v) {
   *(b4*)o = b;
 }
 
+// Thread = output pixel (weights wave-uniform: scalar loads); the block's 256
+// pixels x CP channels are staged in LDS and written back as one contiguous
+// span with 16-byte accesses (a direct thread-per-pixel store strides 8-16 B
+// accesses by the pixel pitch).  The packed weights are zero for channels >= C.
 template <int PH, int PW, typename OT>
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, OT* __restrict__ out,
                                                     const float* __restrict__ w0, int n, int Hin,
                                                     int Win, int H, int W, int C, int CP) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ __attribute__((aligned(16))) OT stage[256 * 48];
+  const int64_t p0 = (int64_t)blockIdx.x * 256;
+  const int64_t gid = p0 + threadIdx.x;
   const int64_t total = (int64_t)n * H * W;
-  if (gid >= total) return;
-  const int ow = (int)(gid % W);
-  const int64_t t = gid / W;
-  const int oh = (int)(t % H);
-  const int b = (int)(t / H);
-  const float* xb = x + (int64_t)b * Hin * Win;
-  // input window rows [oh*PH-1, oh*PH+PH], cols [ow*PW-1, ow*PW+PW]
-  float win[PH + 2][PW + 2];
+  if (gid < total) {
+    const int ow = (int)(gid % W);
+    const int64_t t = gid / W;
+    const int oh = (int)(t % H);
+    const int b = (int)(t / H);
+    const float* xb = x + (int64_t)b * Hin * Win;
+    // input window rows [oh*PH-1, oh*PH+PH], cols [ow*PW-1, ow*PW+PW]
+    float win[PH + 2][PW + 2];
 #pragma unroll
-  for (int r = 0; r < PH + 2; ++r) {
-    const int ir = oh * PH - 1 + r;
+    for (int r = 0; r < PH + 2; ++r) {
+      const int ir = oh * PH - 1 + r;
 #pragma unroll
-    for (int c = 0; c < PW + 2; ++c) {
-      const int ic = ow * PW - 1 + c;
-      win[r][c] = (ir >= 0 && ir < Hin && ic >= 0 && ic < Win) ? xb[(int64_t)ir * Win + ic] : 0.f;
+      for (int c = 0; c < PW + 2; ++c) {
+        const int ic = ow * PW - 1 + c;
+        win[r][c] = (ir >= 0 && ir < Hin && ic >= 0 && ic < Win) ? xb[(int64_t)ir * Win + ic] : 0.f;
+      }
     }
-  }
-  OT* o = out + gid * CP;
-  const float inv = 1.0f / (float)(PH * PW);
-  for (int c4 = 0; c4 < CP; c4 += 4) {
-    float v[4];
+    OT* o = stage + threadIdx.x * CP;
+    const float inv = 1.0f / (float)(PH * PW);
+    for (int c4 = 0; c4 < CP; c4 += 4) {
+      float v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = c4 + u;
-      float s = 0.f;
-      if (c < C) {
-        const float* wc = w0 + c * 9;
+      for (int u = 0; u < 4; ++u) {
+        const float* wc = w0 + (c4 + u) * 9;
         float wr[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) wr[k] = wc[k];
+        float s = 0.f;
 #pragma unroll
         for (int a = 0; a < PH; ++a)
 #pragma unroll
@@ -396,12 +400,18 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
               for (int kx = 0; kx < 3; ++kx) acc = fmaf(win[a + ky][bb + kx], wr[ky * 3 + kx], acc);
             s += fmaxf(acc, 0.f);
           }
-        if (PH * PW > 1) s *= inv;
+        v[u] = (PH * PW > 1) ? s * inv : s;
       }
-      v[u] = s;
+      store4(o + c4, f32x4{v[0], v[1], v[2], v[3]});
     }
-    store4(o + c4, f32x4{v[0], v[1], v[2], v[3]});
   }
+  __syncthreads();
+  // contiguous write-back of the block's valid pixels
+  const int64_t np = (total - p0 < 256) ? total - p0 : 256;
+  const int chunks = (int)(np * CP * (int)sizeof(OT) / 16);
+  const uint4* src = (const uint4*)stage;
+  uint4* dst = (uint4*)(out + p0 * CP);
+  for (int i = threadIdx.x; i < chunks; i += 256) dst[i] = src[i];
 }
 
 // generic pool shape (any PH, PW): same math, input read through L1

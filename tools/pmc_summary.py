@@ -51,16 +51,20 @@ def main():
         out["kernels"][name] = e
     with open(f"profiles/{tag}_pmc_summary.json", "w") as f:
         json.dump(out, f, indent=1)
-    blk = [k for k in out["kernels"] if "block_kernel" in k]
-    if blk:
-        e = out["kernels"][blk[0]]
-        rd = e.get("hbm_read_bytes_corrected")
-        wr = e.get("hbm_write_bytes")
-        res = {"kernel": blk[0], "source": f"profiles/{tag}_pmc_summary.json",
-               "batch_clips_per_launch": batch,
+    # per kernel family (all template instances, weighted by launches) -> the
+    # profiles/pmc_<family>.json that bench.py reads for roofline.traffic
+    for fam in ("block_kernel", "block16_kernel", "conv_gemm_kernel"):
+        ks = [k for k in out["kernels"] if f"::{fam}<" in k and "hbm_read_bytes_corrected" in out["kernels"][k]]
+        if not ks:
+            continue
+        calls = sum(out["kernels"][k]["calls"] for k in ks)
+        rd = sum(out["kernels"][k]["hbm_read_bytes_corrected"] * out["kernels"][k]["calls"] for k in ks) / calls
+        wr = sum(out["kernels"][k].get("hbm_write_bytes", 0.0) * out["kernels"][k]["calls"] for k in ks) / calls
+        res = {"kernel": fam, "instances": ks, "source": f"profiles/{tag}_pmc_summary.json",
+               "batch_clips_per_launch": batch, "launches": calls,
                "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
-               "hbm_bytes_per_launch": (rd or 0) + (wr or 0)}
-        with open("profiles/pmc_block_kernel.json", "w") as f:
+               "hbm_bytes_per_launch": rd + wr}
+        with open(f"profiles/pmc_{fam}.json", "w") as f:
             json.dump(res, f, indent=1)
         print(json.dumps(res, indent=1))
 
