@@ -78,7 +78,7 @@ def cfg_name(cfg):
     return f"res{cfg['n_layers']}-{cfg['n_feature_maps']}maps" if "n_layers" in cfg else "cnn"
 
 
-def load_traffic(kernel, clips_per_launch):
+def load_traffic(kernel, clips_per_launch, model):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC pass
     (profiles/pmc_<kernel>.json, written by tools/pmc_summary.py), or None when no
     pass was taken for that kernel at this launch size."""
@@ -90,7 +90,7 @@ def load_traffic(kernel, clips_per_launch):
             d = json.load(f)
     except Exception:
         return None
-    if d.get("batch_clips_per_launch") != clips_per_launch:
+    if d.get("batch_clips_per_launch") != clips_per_launch or d.get("model") != model:
         return None
     return d.get("hbm_bytes_per_launch")
 
@@ -150,6 +150,31 @@ def train_bench(args, dev, rank, world, barrier):
               flush=True)
 
 
+def _res_geometry(cfg):
+    """(H, W, n_layers, CP) of a res config's block layers (model.py:87-98)."""
+    ph, pw = tuple(cfg.get("res_pool", (1, 1)))
+    C = int(cfg["n_feature_maps"])
+    return 101 // ph, 40 // pw, int(cfg["n_layers"]), 16 * ((C + 15) // 16)
+
+
+def bf16_roofline(cfg, kms, nl, B, model):
+    """HBM roofline of the bf16 block kernel (DESIGN.md 'bf16 block kernel'):
+    algorithmic bytes per launch = clips x (read X [+ read residual on even
+    layers] [+ write Y except in the last layer]) x H*W*CP*2, averaged over the
+    layers of one forward, / the measured average launch time."""
+    H, W, L, CP = _res_geometry(cfg)
+    act = H * W * CP * 2
+    per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1)) / L
+    avg_s = (kms / max(nl, 1)) * 1e-3
+    bw = per_clip * min(B, 4096) / avg_s / 1e9 if nl else None
+    return {"bound": "hbm", "kernel": "honk::res::block16_kernel (dilated 3x3 conv, bf16 MFMA)",
+            "achieved": round(bw, 1) if bw else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(bw / HBM_PEAK_GBS, 4) if bw else None,
+            "traffic": load_traffic("block16_kernel", min(B, 4096), model),
+            "launches": nl, "avg_launch_ms": round(kms / max(nl, 1), 4),
+            "algorithmic_bytes_per_launch": per_clip * min(B, 4096)}
+
+
 def measure_alt_bf16(model, x, args, dev, barrier, hd, _native, orc, cfg, B, world):
     model.honk_precision = "bf16"
     with torch.no_grad():
@@ -173,13 +198,14 @@ def measure_alt_bf16(model, x, args, dev, barrier, hd, _native, orc, cfg, B, wor
                       x[idx].cpu().numpy())
     got = out[idx].cpu().numpy()
     ach = (kfl / max(nl, 1)) / ((kms / max(nl, 1)) * 1e-3) / 1e12 if nl else None
+    # the bf16 block kernel is bound by HBM traffic: algorithmic bytes
+    # per launch = clips x (read X [+ read residual on even layers] [+ write Y
+    # except the last layer]) x H*W*CP*2, averaged over the layers of a forward
     return {"value": round(world * B * args.steps / el, 1), "unit": "clips/s", "dtype": "bf16",
             "ms_per_step": round(el / args.steps * 1e3, 3),
-            "roofline": {"bound": "mfma", "kernel": "honk::res::block16_kernel (dilated 3x3 conv, bf16 MFMA)",
-                         "achieved": round(ach, 2) if ach else None, "peak": BF16_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4) if ach else None,
-                         "avg_launch_ms": round(kms / max(nl, 1), 4),
-                         "traffic": load_traffic("block16_kernel", min(B, 4096))},
+            "roofline": bf16_roofline(cfg, kms, nl, B, args.model),
+            "mfma": {"achieved": round(ach, 2) if ach else None, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4) if ach else None},
             "parity": {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
                        "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()),
                        "sample_clips": len(idx)},
@@ -292,17 +318,16 @@ def main():
                        "per_gpu_batch": B, "global_batch": world * B,
                        "parallelism": f"batch-shard x{world} (no data-path collective)"},
             "model_tflops": round(value * flop_clip / 1e12, 2),
-            "roofline": {"bound": "mfma",
-                         "kernel": (("honk::res::block16_kernel (dilated 3x3 conv, bf16 MFMA)" if bf16 else
-                                     "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)") if is_res else
-                                    "honk::cnn::conv_gemm_kernel (implicit-GEMM conv/linear, fp32 MFMA)"),
-                         "achieved": round(achieved, 2) if achieved else None,
-                         "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4) if achieved else None,
-                         "traffic": (load_traffic("block16_kernel" if bf16 else "block_kernel", min(B, 4096))
-                                     if is_res else None),
-                         "launches": nlaunch, "avg_launch_ms": round(avg_ms, 4),
-                         "flop_per_launch": kflop / max(nlaunch, 1)},
+            "roofline": (bf16_roofline(cfg, kms, nlaunch, B, args.model) if bf16 else
+                         {"bound": "mfma",
+                          "kernel": ("honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)" if is_res else
+                                     "honk::cnn::conv_gemm_kernel (implicit-GEMM conv/linear, fp32 MFMA)"),
+                          "achieved": round(achieved, 2) if achieved else None,
+                          "peak": peak, "unit": "TFLOP/s",
+                          "frac": round(achieved / peak, 4) if achieved else None,
+                          "traffic": load_traffic("block_kernel", min(B, 4096), args.model) if is_res else None,
+                          "launches": nlaunch, "avg_launch_ms": round(avg_ms, 4),
+                          "flop_per_launch": kflop / max(nlaunch, 1)}),
             "parity": {"top1_agreement_vs_oracle": top1, "max_abs_logit_err_vs_oracle_f64": maxerr,
                        "sample_clips": len(idx)},
         }

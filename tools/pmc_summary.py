@@ -1,6 +1,6 @@
 """Summarise rocprofv3 kernel-trace stats + FETCH_SIZE/WRITE_SIZE passes into profiles/.
 
-usage: python tools/pmc_summary.py gpurun_out/prof r1 [batch]
+usage: python tools/pmc_summary.py gpurun_out/prof r1 [clips_per_launch] [model]
 Writes profiles/<tag>_kernel_stats.csv (copy), profiles/<tag>_pmc_summary.json and
 profiles/pmc_block_kernel.json (read by bench.py for roofline.traffic).
 
@@ -30,6 +30,7 @@ def per_kernel(path, counter):
 def main():
     d, tag = sys.argv[1], sys.argv[2]
     batch = int(sys.argv[3]) if len(sys.argv) > 3 else 16384
+    model = sys.argv[4] if len(sys.argv) > 4 else "res15"
     os.makedirs("profiles", exist_ok=True)
     shutil.copy(os.path.join(d, f"{tag}_trace_kernel_stats.csv"), f"profiles/{tag}_kernel_stats.csv")
     fetch = per_kernel(os.path.join(d, f"{tag}_fetch_counter_collection.csv"), "FETCH_SIZE")
@@ -60,7 +61,7 @@ def main():
         calls = sum(out["kernels"][k]["calls"] for k in ks)
         rd = sum(out["kernels"][k]["hbm_read_bytes_corrected"] * out["kernels"][k]["calls"] for k in ks) / calls
         wr = sum(out["kernels"][k].get("hbm_write_bytes", 0.0) * out["kernels"][k]["calls"] for k in ks) / calls
-        res = {"kernel": fam, "instances": ks, "source": f"profiles/{tag}_pmc_summary.json",
+        res = {"kernel": fam, "model": model, "instances": ks, "source": f"profiles/{tag}_pmc_summary.json",
                "batch_clips_per_launch": batch, "launches": calls,
                "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                "hbm_bytes_per_launch": rd + wr}
