@@ -178,6 +178,11 @@ __device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff
   stage_step<NT, MT, NDY, 0>(base, aoff, bcur, acc, a0, a1, wr, lane16, mid);
 }
 
+#ifdef HONK_STAMP
+// diagnostic build only: per-wave cycle split of the block kernels' main loops (s_memtime)
+__device__ unsigned long long honk_stamp_buf[256 * 16 * 8];
+#endif
+
 template <int NT, int MT, bool LAST>
 __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(BlockArgs a) {
   using G = Geo<NT, MT>;
@@ -258,6 +263,16 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
 
   int s = 0;
   f32x4 rv[MT];
+#ifdef HONK_STAMP
+  unsigned long long stamp32[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st32[8];
+#define HONK_STAMP32(x) (x) = __builtin_amdgcn_s_memtime()
+#define HONK_STAMP_VM(DY) { __builtin_amdgcn_s_waitcnt(0xc07f); stamp_vm += __builtin_amdgcn_s_memtime() - st32[2 * (DY)]; }
+  unsigned long long stamp_vm = 0;
+#else
+#define HONK_STAMP_VM(DY) ((void)0)
+#define HONK_STAMP32(x) ((void)0)
+#endif
   while (true) {
     f32x4 acc[MT];
 #pragma unroll
@@ -269,8 +284,11 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   {                                                                                     \
     float* cur = smem + (s & 1) * G::BUF;                                               \
     float* nxt = smem + ((s + 1) & 1) * G::BUF;                                         \
+    HONK_STAMP32(st32[2 * DY]);                                                         \
     if (DY == 0) wait_vmcnt<G::VM_AFTER_GLDS_LAST>(); else wait_vmcnt<G::VM_AFTER_GLDS>(); \
+    HONK_STAMP_VM(DY);                                                                  \
     __builtin_amdgcn_s_barrier();                                                       \
+    HONK_STAMP32(st32[2 * DY + 1]);                                                     \
     auto mid = [&]() {                                                                  \
       if (DY < 2)                                                                       \
         issue_stage<NT, MT>(a, tile, DY + 1, nxt, wave, gpack);                         \
@@ -290,6 +308,7 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
     HONK_STAGE(1)
     HONK_STAGE(2)
 #undef HONK_STAGE
+    HONK_STAMP32(st32[6]);
 
     // epilogue: lane (g, i16) holds out channels c4..c4+3 of pixel i16 of each
     // m-tile: ReLU, residual add, pre-BN store (even layers) and BN store, 16 B
@@ -334,9 +353,20 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
         if (i16 == 0) *(f32x4*)(a.chsum + ((size_t)tile * MW + mg) * G::CP + c4) = csum;
       }
     }
+    HONK_STAMP32(st32[7]);
+#ifdef HONK_STAMP
+    for (int q = 0; q < 7; ++q) stamp32[q] += st32[q + 1] - st32[q];
+#endif
     tile += GR;
     if (tile >= a.ntiles) break;
   }
+#ifdef HONK_STAMP
+  if (lane == 0) {
+    unsigned long long* d = honk_stamp_buf + (size_t)(blockIdx.x * 16 + wave) * 8;
+    for (int q = 0; q < 7; ++q) d[q] = stamp32[q];
+    d[7] = stamp_vm + 1;
+  }
+#endif
 }
 
 // --------------------------------------------------------------------------- //
@@ -353,11 +383,13 @@ __device__ __forceinline__ void store4(__bf16* o, f32x4 v) {
 // pixels x CP channels are staged in LDS and written back as one contiguous
 // span with 16-byte accesses (a direct thread-per-pixel store strides 8-16 B
 // accesses by the pixel pitch).  The packed weights are zero for channels >= C.
-template <int PH, int PW, typename OT>
+template <int PH, int PW, typename OT, bool SPLIT>
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, OT* __restrict__ out,
                                                     const float* __restrict__ w0, int n, int Hin,
                                                     int Win, int H, int W, int C, int CP) {
-  __shared__ __attribute__((aligned(16))) OT stage[256 * 48];
+  // SPLIT (bf16x3 activations): per pixel [hi CP][lo CP] bf16, lo = bf16(v - hi)
+  constexpr int PPX = SPLIT ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) OT stage[256 * 48 * PPX];
   const int64_t p0 = (int64_t)blockIdx.x * 256;
   const int64_t gid = p0 + threadIdx.x;
   const int64_t total = (int64_t)n * H * W;
@@ -378,7 +410,7 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
         win[r][c] = (ir >= 0 && ir < Hin && ic >= 0 && ic < Win) ? xb[(int64_t)ir * Win + ic] : 0.f;
       }
     }
-    OT* o = stage + threadIdx.x * CP;
+    OT* o = stage + threadIdx.x * CP * PPX;
     const float inv = 1.0f / (float)(PH * PW);
     for (int c4 = 0; c4 < CP; c4 += 4) {
       float v[4];
@@ -402,15 +434,22 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
           }
         v[u] = (PH * PW > 1) ? s * inv : s;
       }
-      store4(o + c4, f32x4{v[0], v[1], v[2], v[3]});
+      const f32x4 vv = {v[0], v[1], v[2], v[3]};
+      store4(o + c4, vv);
+      if constexpr (SPLIT) {
+        f32x4 lo;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) lo[u] = vv[u] - (float)(OT)vv[u];
+        store4(o + CP + c4, lo);
+      }
     }
   }
   __syncthreads();
   // contiguous write-back of the block's valid pixels
   const int64_t np = (total - p0 < 256) ? total - p0 : 256;
-  const int chunks = (int)(np * CP * (int)sizeof(OT) / 16);
+  const int chunks = (int)(np * CP * PPX * (int)sizeof(OT) / 16);
   const uint4* src = (const uint4*)stage;
-  uint4* dst = (uint4*)(out + p0 * CP);
+  uint4* dst = (uint4*)(out + p0 * CP * PPX);
   for (int i = threadIdx.x; i < chunks; i += 256) dst[i] = src[i];
 }
 
@@ -565,7 +604,7 @@ struct Layout {
   int C, CP, NT, L, NL, prec, KS16;
   int Hin, Win, H, W, ph, pw;
   size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, off_frag16, frag16_floats,
-      off_bias16, total;
+      off_fragx3, fragx3_floats, off_bias16, total;
 };
 
 static size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
@@ -599,15 +638,18 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   L->off_wout = L->off_bn + round64((size_t)2 * L->CP * L->L);
   L->off_bout = L->off_wout + round64((size_t)L->NL * L->C);
   L->off_zeros = L->off_bout + round64((size_t)L->NL);
-  // bf16 B fragments [L][3][KS][NT][64][8] (bf16) for the HONK_PREC_BF16 kernel
+  // bf16 weight fragments per layer (layout G16::wfrag) for HONK_PREC_BF16 and the
+  // hi/lo pairs for HONK_PREC_BF16X3
   L->KS16 = (6 * L->NT + 3) / 4;
   L->off_frag16 = L->off_zeros + 64;
-  L->frag16_floats = (size_t)3 * L->KS16 * L->NT * 64 * 8 / 2;
+  L->frag16_floats = (size_t)g16_frag_bytes(L->NT, 1) / 4;
+  L->off_fragx3 = L->off_frag16 + L->frag16_floats * L->L;
+  L->fragx3_floats = (size_t)g16_frag_bytes(L->NT, 2) / 4;
   // folded input-BN bias [L][16 classes][CP] for the bf16 kernel
-  L->off_bias16 = L->off_frag16 + L->frag16_floats * L->L;
+  L->off_bias16 = L->off_fragx3 + L->fragx3_floats * L->L;
   L->total = L->off_bias16 + (size_t)16 * L->CP * L->L;
   L->prec = d->precision;
-  if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16)
+  if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16 && L->prec != HONK_PREC_BF16X3)
     return fail(HONK_ERR_ARG, "unknown precision %d", d->precision);
   return HONK_OK;
 }
@@ -650,9 +692,11 @@ static Plan plan_block(const Layout& L) {
 }
 
 // bf16 kernel plan: 8 waves x MT m-tiles; MT is the largest whose 3-buffer ring
-// plus the layer's weights fit the 160 KiB LDS (NT = 3 -> 3, else 4)
-static Plan plan_block16(const Layout& L) {
-  const int MT = (L.NT == 3) ? 3 : 4;
+// plus the layer's weights fit the 160 KiB LDS (SP = 1: NT = 3 -> 3, else 4;
+// SP = 2: NT = 3 -> 1, NT = 2 -> 2, NT = 1 -> 4)
+static Plan plan_block16(const Layout& L, int SP) {
+  int MT = 4;
+  while (MT > 1 && g16_lds_bytes(L.NT, MT, SP) > 160 * 1024) --MT;
   const int MP = 128 * MT;
   const int thmax = MP / L.W;  // >= 1: make_layout bounds W
   const int nb = (L.H + thmax - 1) / thmax;
@@ -660,26 +704,32 @@ static Plan plan_block16(const Layout& L) {
   return Plan{L.NT, MT, th, nb};
 }
 
-template <int NT, int MT>
+template <int NT, int MT, int SP>
 static int launch_block16(const Block16Args& a, hipStream_t st) {
-  using G = G16<NT, MT>;
+  using G = G16<NT, MT, SP>;
   static_assert(G::LDS <= 160 * 1024, "LDS");
   int grid = cu_count();
   if (grid > a.ntiles) grid = a.ntiles;
   const dim3 gd(grid), bd(G::NTHREADS);
-  if (a.chsum && a.res) hipLaunchKernelGGL((block16_kernel<NT, MT, true, true>), gd, bd, 0, st, a);
-  else if (a.chsum) hipLaunchKernelGGL((block16_kernel<NT, MT, true, false>), gd, bd, 0, st, a);
-  else if (a.res) hipLaunchKernelGGL((block16_kernel<NT, MT, false, true>), gd, bd, 0, st, a);
-  else hipLaunchKernelGGL((block16_kernel<NT, MT, false, false>), gd, bd, 0, st, a);
+  if (a.chsum && a.res) hipLaunchKernelGGL((block16_kernel<NT, MT, SP, true, true>), gd, bd, 0, st, a);
+  else if (a.chsum) hipLaunchKernelGGL((block16_kernel<NT, MT, SP, true, false>), gd, bd, 0, st, a);
+  else if (a.res) hipLaunchKernelGGL((block16_kernel<NT, MT, SP, false, true>), gd, bd, 0, st, a);
+  else hipLaunchKernelGGL((block16_kernel<NT, MT, SP, false, false>), gd, bd, 0, st, a);
   HONK_LAUNCH_CHECK("res block16_kernel");
   return HONK_OK;
 }
 
-static int dispatch_block16(const Plan& p, const Block16Args& a, hipStream_t st) {
-  if (p.NT == 1 && p.MT == 4) return launch_block16<1, 4>(a, st);
-  if (p.NT == 2 && p.MT == 4) return launch_block16<2, 4>(a, st);
-  if (p.NT == 3 && p.MT == 3) return launch_block16<3, 3>(a, st);
-  return fail(HONK_ERR_UNSUPPORTED, "no bf16 block kernel for NT=%d MT=%d", p.NT, p.MT);
+static int dispatch_block16(const Plan& p, int SP, const Block16Args& a, hipStream_t st) {
+  if (SP == 1) {
+    if (p.NT == 1 && p.MT == 4) return launch_block16<1, 4, 1>(a, st);
+    if (p.NT == 2 && p.MT == 4) return launch_block16<2, 4, 1>(a, st);
+    if (p.NT == 3 && p.MT == 3) return launch_block16<3, 3, 1>(a, st);
+  } else {
+    if (p.NT == 1 && p.MT == 4) return launch_block16<1, 4, 2>(a, st);
+    if (p.NT == 2 && p.MT == 2) return launch_block16<2, 2, 2>(a, st);
+    if (p.NT == 3 && p.MT == 1) return launch_block16<3, 1, 2>(a, st);
+  }
+  return fail(HONK_ERR_UNSUPPORTED, "no bf16 block kernel for NT=%d MT=%d SP=%d", p.NT, p.MT, SP);
 }
 
 template <int NT, int MT>
@@ -705,20 +755,21 @@ static int dispatch_block(const Plan& p, const BlockArgs& a, hipStream_t st) {
   return fail(HONK_ERR_UNSUPPORTED, "no block kernel for NT=%d MT=%d", p.NT, p.MT);
 }
 
-template <typename OT>
+template <typename OT, bool SPLIT = false>
 static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w0, int64_t n,
                         hipStream_t st) {
   const int64_t total = n * L.H * L.W;
   const int blocks = (int)cdiv(total, 256);
-#define HONK_C0(PH, PW)                                                                        \
-  if (L.ph == PH && L.pw == PW) {                                                              \
-    hipLaunchKernelGGL((conv0_kernel<PH, PW, OT>), dim3(blocks), dim3(256), 0, st, x, out, w0, \
-                       (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                             \
-    HONK_LAUNCH_CHECK("res conv0_kernel");                                                     \
-    return HONK_OK;                                                                            \
+#define HONK_C0(PH, PW)                                                                               \
+  if (L.ph == PH && L.pw == PW) {                                                                     \
+    hipLaunchKernelGGL((conv0_kernel<PH, PW, OT, SPLIT>), dim3(blocks), dim3(256), 0, st, x, out, w0, \
+                       (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                                    \
+    HONK_LAUNCH_CHECK("res conv0_kernel");                                                            \
+    return HONK_OK;                                                                                   \
   }
   HONK_C0(1, 1) HONK_C0(2, 2) HONK_C0(4, 3)
 #undef HONK_C0
+  if (SPLIT) return fail(HONK_ERR_UNSUPPORTED, "bf16x3: avg-pool %dx%d has no conv0 kernel", L.ph, L.pw);
   hipLaunchKernelGGL((conv0_generic_kernel<OT>), dim3(blocks), dim3(256), 0, st, x, out, w0, (int)n, L.Hin,
                      L.Win, L.H, L.W, L.C, L.CP, L.ph, L.pw);
   HONK_LAUNCH_CHECK("res conv0_generic_kernel");
@@ -731,18 +782,20 @@ static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w
 // buffer X suffice; each layer writes exactly one tensor.
 static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* packed, const float* x,
                         float* logits, int64_t batch, int64_t chunk, void* workspace, hipStream_t st) {
-  const size_t act = (size_t)chunk * L.H * L.W * L.CP;
+  const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;  // bf16 elements per channel value
+  const size_t act = (size_t)chunk * L.H * L.W * L.CP * SP;
   __bf16* R = (__bf16*)workspace;
   __bf16* X = R + act;
   float* chsum = (float*)(R + 2 * act);
-  const Plan p = plan_block16(L);
+  const Plan p = plan_block16(L, SP);
   const double layer_flop_per_clip = 2.0 * L.H * L.W * L.C * L.C * 9;
   if (L.L == 0) return fail(HONK_ERR_UNSUPPORTED, "bf16 path needs n_layers >= 1");
   int rc;
   for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
     const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
     if ((int64_t)n * p.nbands > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
-    rc = launch_conv0(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+    rc = (SP == 2) ? launch_conv0<__bf16, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+                   : launch_conv0<__bf16, false>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
     if (rc) return rc;
     for (int i = 1; i <= L.L; ++i) {
       const bool even = (i % 2) == 0;
@@ -750,7 +803,8 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       a.in = even ? X : R;
       a.res = even ? R : nullptr;
       a.out = (i == L.L) ? nullptr : (even ? R : X);
-      a.bfrag = (const uint4*)(packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
+      a.bfrag = (const uint4*)(SP == 2 ? packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats
+                                       : packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
       a.bias = packed + L.off_bias16 + (size_t)16 * L.CP * (i - 1);
       a.chsum = (i == L.L) ? chsum : nullptr;
       a.H = L.H;
@@ -760,7 +814,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       a.nbands = p.nbands;
       a.ntiles = (int)(n * p.nbands);
       TimedLaunch tl(st, layer_flop_per_clip * (double)n);
-      rc = dispatch_block16(p, a, st);
+      rc = dispatch_block16(p, SP, a, st);
       tl.done(st);
       if (rc) return rc;
 #ifdef HONK_STAMP
@@ -809,9 +863,10 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   Layout L;
   if (make_layout(d, &L) != HONK_OK || batch < 1) return 0;
   const int64_t ch = chunk_clips(L, batch);
-  if (L.prec == HONK_PREC_BF16) {
-    const Plan p = plan_block16(L);
-    return (size_t)2 * ch * L.H * L.W * L.CP * 2 + (size_t)ch * p.nbands * 8 * L.CP * sizeof(float);
+  if (L.prec != HONK_PREC_F32) {
+    const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;
+    const Plan p = plan_block16(L, SP);
+    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * p.nbands * 8 * L.CP * sizeof(float);
   }
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
@@ -842,7 +897,9 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
     const float* in_bn = (i > 0) ? packed + L.off_bn + (size_t)2 * L.CP * (i - 1) : nullptr;
     const int n16 = 3 * L.KS16 * L.NT * 64 * 8;
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
-                       (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16);
+                       (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16, 1);
+    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
+                       (__bf16*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, L.KS16, 2);
     HONK_LAUNCH_CHECK("pack_block16");
     hipLaunchKernelGGL(pack_bias16_kernel, dim3(cdiv(16 * L.CP, 256)), dim3(256), 0, st, t[1 + i],
                        in_bn ? in_bn + L.CP : nullptr, packed + L.off_bias16 + (size_t)16 * L.CP * i, L.C, L.CP);
@@ -875,7 +932,7 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
     return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
   hipStream_t st = (hipStream_t)stream;
   const int64_t chunk = chunk_clips(L, batch);
-  if (L.prec == HONK_PREC_BF16) return forward_bf16(L, d, packed, x, logits, batch, chunk, workspace, st);
+  if (L.prec != HONK_PREC_F32) return forward_bf16(L, d, packed, x, logits, batch, chunk, workspace, st);
   const size_t act = (size_t)chunk * L.H * L.W * L.CP;
   float* R = (float*)workspace;
   float* X[2] = {R + act, R + 2 * act};
@@ -910,6 +967,26 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
       rc = dispatch_block(p, a, st);
       tl.done(st);
       if (rc) return rc;
+#ifdef HONK_STAMP
+      {
+        static unsigned long long h[256 * 16 * 8];
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(honk_stamp_buf), sizeof(h));
+        double sum[8] = {0};
+        int nw = 0;
+        for (int w = 0; w < 256 * 16; ++w)
+          if (h[w * 8 + 7]) {
+            double tot = 0;
+            for (int q = 0; q < 7; ++q) tot += (double)h[w * 8 + q];
+            for (int q = 0; q < 7; ++q) sum[q] += (double)h[w * 8 + q] / tot;
+            sum[7] += (double)(h[w * 8 + 7] - 1) / tot;
+            ++nw;
+          }
+        if (nw)
+          fprintf(stderr, "stamp32 layer %d: w0 %.3f c0 %.3f w1 %.3f c1 %.3f w2 %.3f c2 %.3f epi %.3f (vmcnt part of waits %.3f)\n", i,
+                  sum[0] / nw, sum[1] / nw, sum[2] / nw, sum[3] / nw, sum[4] / nw, sum[5] / nw, sum[6] / nw, sum[7] / nw);
+      }
+#endif
     }
     if (L.L == 0) {  // no block layer: mean of the conv0 output
       hipLaunchKernelGGL(tail_kernel, dim3((unsigned)n), dim3(L.CP * (256 / L.CP)), 0, st, R,

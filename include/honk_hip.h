@@ -43,13 +43,17 @@ typedef struct honk_res_desc {
   int32_t use_dilation;   /* config["use_dilation"]: conv{i} dilation 2**((i-1)//3) */
   int32_t pool_h, pool_w; /* config["res_pool"], or 0,0 when absent              */
   int32_t height, width;  /* input frames x MFCC coefficients (101, 40)          */
-  int32_t precision;      /* HONK_PREC_F32 (IEEE fp32, 1e-4 parity) or
+  int32_t precision;      /* HONK_PREC_F32 (IEEE fp32 MFMA, 1e-4 parity),
                              HONK_PREC_BF16 (bf16 activations/weights, fp32
-                             accumulate; top-1 parity) -- same packed buffer   */
+                             accumulate; top-1 parity) or HONK_PREC_BF16X3
+                             (fp32 values as bf16 hi + lo pairs, products
+                             hi*hi + hi*lo + lo*hi on bf16 MFMA, fp32
+                             accumulate; 1e-4 parity) -- same packed buffer  */
 } honk_res_desc;
 
 #define HONK_PREC_F32 0
 #define HONK_PREC_BF16 1
+#define HONK_PREC_BF16X3 2
 
 /* number of floats of the packed (kernel-layout) weight buffer */
 size_t honk_res_packed_floats(const honk_res_desc* d);
