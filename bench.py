@@ -41,9 +41,11 @@ def parse():
     p.add_argument("--model", default="res15")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--precision", default="f32", choices=["f32", "bf16"],
-                   help="res path arithmetic: f32 (exact, 1e-4 parity) or bf16 (top-1 parity)")
-    p.add_argument("--no-alt", action="store_true", help="skip the extra bf16-mode measurement of res models")
+    p.add_argument("--precision", default="bf16x3", choices=["bf16x3", "f32", "bf16"],
+                   help="res path arithmetic: bf16x3 (fp32 values as bf16 hi/lo pairs, 3 bf16 MFMA products, "
+                        "fp32 accumulation; 1e-4 parity), f32 (fp32 MFMA; 1e-4 parity) or bf16 (top-1 parity)")
+    p.add_argument("--no-alt", action="store_true",
+                   help="skip the extra measurements of the other res precision modes")
     p.add_argument("--e2e", action="store_true",
                    help="serving pipeline: int16-scaled PCM [B,16000] in HBM -> GPU MFCC -> model -> logits")
     p.add_argument("--train", action="store_true",
@@ -157,26 +159,53 @@ def _res_geometry(cfg):
     return 101 // ph, 40 // pw, int(cfg["n_layers"]), 16 * ((C + 15) // 16)
 
 
-def bf16_roofline(cfg, kms, nl, B, model):
-    """HBM roofline of the bf16 block kernel (DESIGN.md 'bf16 block kernel'):
-    algorithmic bytes per launch = clips x (read X [+ read residual on even
-    layers] [+ write Y except in the last layer]) x H*W*CP*2, averaged over the
-    layers of one forward, / the measured average launch time."""
-    H, W, L, CP = _res_geometry(cfg)
-    act = H * W * CP * 2
-    per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1)) / L
+PREC_NOTES = {
+    "bf16x3": "fp32 values carried as bf16 (hi, lo) pairs; products hi*hi + hi*lo + lo*hi on bf16 MFMA, fp32 "
+              "accumulation; meets the fp32 1e-4 logit parity bar (tests/test_gpu_bf16x3.py)",
+    "f32": "IEEE fp32 on v_mfma_f32_16x16x4_f32; 1e-4 logit parity",
+    "bf16": "bf16 activations/weights, fp32 accumulation; top-1 parity only (reduced precision vs the fp32 "
+            "reference), so never the headline",
+}
+
+
+def res_roofline(prec, cfg, kms, nl, kfl, B, model):
+    """Roofline of the dominant res kernel for a precision mode.
+
+    f32: MFMA-bound -- algorithmic FLOP per launch / mean launch time vs the fp32
+    MFMA peak.  bf16 / bf16x3 (block16_kernel, SP = 1 / 2): HBM-bound --
+    algorithmic bytes per launch = clips x (read X [+ read residual on even layers]
+    [+ write Y except the last layer]) x H*W*CP*2*SP, averaged over the layers of
+    one forward, / the mean launch time."""
     avg_s = (kms / max(nl, 1)) * 1e-3
-    bw = per_clip * min(B, 4096) / avg_s / 1e9 if nl else None
-    return {"bound": "hbm", "kernel": "honk::res::block16_kernel (dilated 3x3 conv, bf16 MFMA)",
+    clips = min(B, 4096)
+    if prec == "f32":
+        ach = (kfl / max(nl, 1)) / avg_s / 1e12 if nl else None
+        return {"bound": "mfma", "kernel": "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)",
+                "achieved": round(ach, 2) if ach else None, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None,
+                "traffic": load_traffic("block_kernel", clips, model),
+                "launches": nl, "avg_launch_ms": round(kms / max(nl, 1), 4),
+                "flop_per_launch": kfl / max(nl, 1)}
+    sp = 2 if prec == "bf16x3" else 1
+    H, W, L, CP = _res_geometry(cfg)
+    act = H * W * CP * 2 * sp
+    per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1)) / L
+    bw = per_clip * clips / avg_s / 1e9 if nl else None
+    mf = (kfl * (3 if sp == 2 else 1) / max(nl, 1)) / avg_s / 1e12 if nl else None
+    return {"bound": "hbm", "kernel": f"honk::res::block16_kernel<..., SP={sp}> (dilated 3x3 conv, bf16 MFMA)",
             "achieved": round(bw, 1) if bw else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(bw / HBM_PEAK_GBS, 4) if bw else None,
-            "traffic": load_traffic("block16_kernel", min(B, 4096), model),
+            "traffic": load_traffic(f"block16_kernel_sp{sp}", clips, model),
             "launches": nl, "avg_launch_ms": round(kms / max(nl, 1), 4),
-            "algorithmic_bytes_per_launch": per_clip * min(B, 4096)}
+            "algorithmic_bytes_per_launch": per_clip * clips,
+            "mfma": {"executed_bf16_tflops": round(mf, 2) if mf else None, "peak": BF16_MFMA_PEAK_TFLOPS,
+                     "frac": round(mf / BF16_MFMA_PEAK_TFLOPS, 4) if mf else None}}
 
 
-def measure_alt_bf16(model, x, args, dev, barrier, hd, _native, orc, cfg, B, world):
-    model.honk_precision = "bf16"
+def measure_mode(prec, model, x, args, dev, barrier, hd, _native, orc, cfg, B, world):
+    """The same res workload in another precision mode (reported beside the headline)."""
+    keep = model.honk_precision
+    model.honk_precision = prec
     with torch.no_grad():
         for _ in range(max(1, args.warmup)):
             model(x)
@@ -191,26 +220,19 @@ def measure_alt_bf16(model, x, args, dev, barrier, hd, _native, orc, cfg, B, wor
         barrier()
         kms, nl, kfl = _native.timing_read()
         _native.timing_enable(False)
-    model.honk_precision = "f32"
+    model.honk_precision = keep
     el = hd.max_over_ranks(t1 - t0, device=dev)
     idx = list(range(0, B, max(1, B // 32)))[:32]
     ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}, cfg,
                       x[idx].cpu().numpy())
     got = out[idx].cpu().numpy()
-    ach = (kfl / max(nl, 1)) / ((kms / max(nl, 1)) * 1e-3) / 1e12 if nl else None
-    # the bf16 block kernel is bound by HBM traffic: algorithmic bytes
-    # per launch = clips x (read X [+ read residual on even layers] [+ write Y
-    # except the last layer]) x H*W*CP*2, averaged over the layers of a forward
-    return {"value": round(world * B * args.steps / el, 1), "unit": "clips/s", "dtype": "bf16",
+    return {"value": round(world * B * args.steps / el, 1), "unit": "clips/s", "dtype": prec,
             "ms_per_step": round(el / args.steps * 1e3, 3),
-            "roofline": bf16_roofline(cfg, kms, nl, B, args.model),
-            "mfma": {"achieved": round(ach, 2) if ach else None, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4) if ach else None},
+            "roofline": res_roofline(prec, cfg, kms, nl, kfl, B, args.model),
             "parity": {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
                        "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()),
                        "sample_clips": len(idx)},
-            "note": "bf16 activations/weights, fp32 accumulation; reduced precision vs the fp32 reference, "
-                    "so reported beside the fp32 headline (value), not as it"}
+            "note": PREC_NOTES[prec]}
 
 
 def main():
@@ -277,10 +299,10 @@ def main():
         _native.timing_enable(False)
     elapsed = hd.max_over_ranks(t1 - t0, device=dev)  # whole-job time = slowest rank
 
-    bf16 = is_res and args.precision == "bf16"
-    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
-    # top-1 agreement of the GPU logits with the float64 oracle on a few clips
-    idx = [0, B // 3, B - 1] if not bf16 else list(range(0, B, max(1, B // 32)))[:32]
+    prec = args.precision if is_res else "f32"
+    peak = FP32_MFMA_PEAK_TFLOPS
+    # top-1 agreement / max logit error of the GPU logits vs the float64 oracle on a sample
+    idx = list(range(0, B, max(1, B // 32)))[:32]
     xs = (ap.compute_mfccs_batch(x[idx]) if args.e2e else x[idx]).cpu().numpy()
     ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()},
                       cfg, xs)
@@ -288,11 +310,13 @@ def main():
     top1 = float(np.mean(np.argmax(ref, 1) == np.argmax(got, 1)))
     maxerr = float(np.abs(ref - got).max())
 
-    # secondary measurement: the same workload in the bf16 precision mode (C3/C4),
-    # reported beside -- never instead of -- the fp32 headline
-    alt = None
-    if is_res and args.precision == "f32" and not args.no_alt and not args.e2e:
-        alt = measure_alt_bf16(model, x, args, dev, barrier, hd, _native, orc, cfg, B, world)
+    # the other precision modes of the same workload, reported beside the headline
+    alts = {}
+    if is_res and not args.no_alt and not args.e2e:
+        for other in ("f32", "bf16"):
+            if other != prec:
+                alts[f"{other}_mode"] = measure_mode(other, model, x, args, dev, barrier, hd, _native, orc, cfg,
+                                                     B, world)
 
     total = world * B * args.steps
     value = total / elapsed
@@ -311,28 +335,27 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if (is_res and args.precision == "bf16") else "f32",
+            "dtype": prec,
+            "precision_note": PREC_NOTES[prec],
             "data": "synthetic N(0,1) [B,101,40] fp32 MFCC-shaped input resident in HBM; random-init weights",
             "config": {"workload": ("PCM -> GPU MFCC -> " if args.e2e else "")
                                    + WORKLOADS.get(args.model, f"{args.model} eval forward"),
                        "per_gpu_batch": B, "global_batch": world * B,
                        "parallelism": f"batch-shard x{world} (no data-path collective)"},
             "model_tflops": round(value * flop_clip / 1e12, 2),
-            "roofline": (bf16_roofline(cfg, kms, nlaunch, B, args.model) if bf16 else
+            "roofline": (res_roofline(prec, cfg, kms, nlaunch, kflop, B, args.model) if is_res else
                          {"bound": "mfma",
-                          "kernel": ("honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)" if is_res else
-                                     "honk::cnn::conv_gemm_kernel (implicit-GEMM conv/linear, fp32 MFMA)"),
+                          "kernel": "honk::cnn::conv_gemm_kernel (implicit-GEMM conv/linear, fp32 MFMA)",
                           "achieved": round(achieved, 2) if achieved else None,
                           "peak": peak, "unit": "TFLOP/s",
                           "frac": round(achieved / peak, 4) if achieved else None,
-                          "traffic": load_traffic("block_kernel", min(B, 4096), args.model) if is_res else None,
+                          "traffic": None,
                           "launches": nlaunch, "avg_launch_ms": round(avg_ms, 4),
                           "flop_per_launch": kflop / max(nlaunch, 1)}),
             "parity": {"top1_agreement_vs_oracle": top1, "max_abs_logit_err_vs_oracle_f64": maxerr,
                        "sample_clips": len(idx)},
         }
-        if alt is not None:
-            res["bf16_mode"] = alt
+        res.update(alts)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         print(json.dumps(res), flush=True)

@@ -695,13 +695,13 @@ static Plan plan_block(const Layout& L) {
 // plus the layer's weights fit the 160 KiB LDS (SP = 1: NT = 3 -> 3, else 4;
 // SP = 2: NT = 3 -> 1, NT = 2 -> 2, NT = 1 -> 4)
 static Plan plan_block16(const Layout& L, int SP) {
-  int MT = 4;
-  while (MT > 1 && g16_lds_bytes(L.NT, MT, SP) > 160 * 1024) --MT;
-  const int MP = 128 * MT;
+  int MT8 = 4;  // m-tiles per wave at 8 waves; the tile is 128 * MT8 pixels
+  while (MT8 > 1 && g16_lds_bytes(L.NT, 128 * MT8, SP) > 160 * 1024) --MT8;
+  const int MP = 128 * MT8;
   const int thmax = MP / L.W;  // >= 1: make_layout bounds W
   const int nb = (L.H + thmax - 1) / thmax;
   const int th = (L.H + nb - 1) / nb;
-  return Plan{L.NT, MT, th, nb};
+  return Plan{L.NT, MP / (16 * g16_nw(SP)), th, nb};
 }
 
 template <int NT, int MT, int SP>
@@ -720,14 +720,15 @@ static int launch_block16(const Block16Args& a, hipStream_t st) {
 }
 
 static int dispatch_block16(const Plan& p, int SP, const Block16Args& a, hipStream_t st) {
+  constexpr int B = HONK_B16_NW, X = HONK_X3_NW;
   if (SP == 1) {
-    if (p.NT == 1 && p.MT == 4) return launch_block16<1, 4, 1>(a, st);
-    if (p.NT == 2 && p.MT == 4) return launch_block16<2, 4, 1>(a, st);
-    if (p.NT == 3 && p.MT == 3) return launch_block16<3, 3, 1>(a, st);
+    if (p.NT == 1 && p.MT == 32 / B) return launch_block16<1, 32 / B, 1>(a, st);
+    if (p.NT == 2 && p.MT == 32 / B) return launch_block16<2, 32 / B, 1>(a, st);
+    if (p.NT == 3 && p.MT == 24 / B) return launch_block16<3, 24 / B, 1>(a, st);
   } else {
-    if (p.NT == 1 && p.MT == 4) return launch_block16<1, 4, 2>(a, st);
-    if (p.NT == 2 && p.MT == 2) return launch_block16<2, 2, 2>(a, st);
-    if (p.NT == 3 && p.MT == 1) return launch_block16<3, 1, 2>(a, st);
+    if (p.NT == 1 && p.MT == 32 / X) return launch_block16<1, 32 / X, 2>(a, st);
+    if (p.NT == 2 && p.MT == 16 / X) return launch_block16<2, 16 / X, 2>(a, st);
+    if (p.NT == 3 && p.MT == 8 / X) return launch_block16<3, 8 / X, 2>(a, st);
   }
   return fail(HONK_ERR_UNSUPPORTED, "no bf16 block kernel for NT=%d MT=%d SP=%d", p.NT, p.MT, SP);
 }
@@ -822,23 +823,24 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         static unsigned long long h[256 * 8 * 8];
         (void)hipStreamSynchronize(st);
         (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(honk_stamp_buf), sizeof(h));
-        double sum[7] = {0};
+        double sum[8] = {0};
         int nw = 0;
         for (int w = 0; w < 256 * 8; ++w)
           if (h[w * 8 + 7]) {
             for (int q = 0; q < 7; ++q) sum[q] += (double)h[w * 8 + q];
+            sum[7] += (double)(h[w * 8 + 7] - 1);
             ++nw;
           }
         if (nw)
-          fprintf(stderr, "stamp layer %d dil %d: w0 %.3f c0 %.3f w1 %.3f c1 %.3f w2 %.3f c2 %.3f (of %.0f)\n", i, a.dil,
-                  sum[0] / sum[6], sum[1] / sum[6], sum[2] / sum[6], sum[3] / sum[6], sum[4] / sum[6],
-                  sum[5] / sum[6], sum[6] / nw);
+          fprintf(stderr, "stamp layer %d dil %d: w0 %.3f c0 %.3f w1 %.3f c1 %.3f w2 %.3f c2 %.3f (vmcnt %.3f) (of %.0f)\n",
+                  i, a.dil, sum[0] / sum[6], sum[1] / sum[6], sum[2] / sum[6], sum[3] / sum[6], sum[4] / sum[6],
+                  sum[5] / sum[6], sum[7] / sum[6], sum[6] / nw);
       }
 #endif
     }
     const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
     hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
-                       packed + L.off_bout, logits + c0 * L.NL, p.nbands * 8, L.H * L.W, L.C, L.CP, L.NL,
+                       packed + L.off_bout, logits + c0 * L.NL, p.nbands * g16_nw(SP), L.H * L.W, L.C, L.CP, L.NL,
                        bn_last, bn_last + L.CP);
     HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16)");
   }
@@ -866,7 +868,7 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   if (L.prec != HONK_PREC_F32) {
     const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;
     const Plan p = plan_block16(L, SP);
-    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * p.nbands * 8 * L.CP * sizeof(float);
+    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * p.nbands * g16_nw(SP) * L.CP * sizeof(float);
   }
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);

@@ -54,8 +54,17 @@ def main():
         json.dump(out, f, indent=1)
     # per kernel family (all template instances, weighted by launches) -> the
     # profiles/pmc_<family>.json that bench.py reads for roofline.traffic
-    for fam in ("block_kernel", "block16_kernel", "conv_gemm_kernel"):
-        ks = [k for k in out["kernels"] if f"::{fam}<" in k and "hbm_read_bytes_corrected" in out["kernels"][k]]
+    def family(k):
+        if "::block16_kernel<" in k:  # split by SP (3rd template argument): sp1 = bf16, sp2 = bf16x3
+            return "block16_kernel_sp" + k.split("<")[1].split(",")[2].strip()
+        for fam in ("block_kernel", "conv_gemm_kernel"):
+            if f"::{fam}<" in k:
+                return fam
+        return None
+
+    fams = sorted({family(k) for k in out["kernels"]} - {None})
+    for fam in fams:
+        ks = [k for k in out["kernels"] if family(k) == fam and "hbm_read_bytes_corrected" in out["kernels"][k]]
         if not ks:
             continue
         calls = sum(out["kernels"][k]["calls"] for k in ks)
