@@ -266,9 +266,10 @@ def main():
     cfg = dict(hm.find_config(args.model))
     torch.manual_seed(0)
     model = hm.find_model(args.model)(cfg).eval().to(dev)
-    if args.model.startswith("res"):
-        model.honk_precision = args.precision
     is_res = args.model.startswith("res")
+    if not is_res and args.precision == "bf16":
+        raise SystemExit("cnn models: --precision f32 or bf16x3")
+    model.honk_precision = args.precision
     B = args.batch or (131072 if is_res else 65536)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(B, 101, 40, device=dev, generator=g)  # resident in HBM before timing
@@ -299,8 +300,9 @@ def main():
         _native.timing_enable(False)
     elapsed = hd.max_over_ranks(t1 - t0, device=dev)  # whole-job time = slowest rank
 
-    prec = args.precision if is_res else "f32"
-    peak = FP32_MFMA_PEAK_TFLOPS
+    prec = args.precision
+    # cnn bf16x3: each algorithmic MAC is 3 bf16 MFMA products -> effective peak = bf16 peak / 3
+    peak = FP32_MFMA_PEAK_TFLOPS if prec == "f32" else BF16_MFMA_PEAK_TFLOPS / 3
     # top-1 agreement / max logit error of the GPU logits vs the float64 oracle on a sample
     idx = list(range(0, B, max(1, B // 32)))[:32]
     xs = (ap.compute_mfccs_batch(x[idx]) if args.e2e else x[idx]).cpu().numpy()
@@ -345,7 +347,10 @@ def main():
             "model_tflops": round(value * flop_clip / 1e12, 2),
             "roofline": (res_roofline(prec, cfg, kms, nlaunch, kflop, B, args.model) if is_res else
                          {"bound": "mfma",
-                          "kernel": "honk::cnn::conv_gemm_kernel (implicit-GEMM conv/linear, fp32 MFMA)",
+                          "kernel": ("honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM conv/linear, fp32 MFMA)"
+                                     if prec == "f32" else
+                                     "honk::cnn::conv_gemm_kernel<.., X3=true> (implicit-GEMM conv/linear, "
+                                     "3 bf16 MFMA products per MAC; peak = bf16 peak / 3)"),
                           "achieved": round(achieved, 2) if achieved else None,
                           "peak": peak, "unit": "TFLOP/s",
                           "frac": round(achieved / peak, 4) if achieved else None,

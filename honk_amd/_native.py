@@ -31,7 +31,7 @@ class CnnDesc(ctypes.Structure):
         "height", "width", "n_labels",
         "c1_out", "c1_kh", "c1_kw", "c1_sh", "c1_sw", "p1_h", "p1_w",
         "has_conv2", "c2_out", "c2_kh", "c2_kw", "c2_sh", "c2_sw", "p2_h", "p2_w",
-        "has_lin", "dnn1", "dnn2", "dnn1_relu")]
+        "has_lin", "dnn1", "dnn2", "dnn1_relu", "precision")]
 
 
 # name -> (restype, argtypes)

@@ -44,10 +44,27 @@ struct GemmArgs {
 // POOL2: rows are ordered (clip, ph, pw, 2x2 member) so the four members of a
 // max-pool window sit in 4 adjacent lanes: the epilogue max-reduces them with
 // two lane swaps and stores only the pooled value (nn.MaxPool2d((2,2)) fused).
-template <bool POOL2>
+//
+// X3 (bf16x3 mode): the same GEMM with every operand split at staging time into
+// bf16 (hi, lo) = (bf16(v), bf16(v - hi)), stored k-contiguous ([m][k], [n][k])
+// so a lane's 8 consecutive k are one 16-byte MFMA fragment, and each 32-deep
+// slice is ONE v_mfma_f32_16x16x32_bf16 step of 3 products (hi*hi + hi*lo +
+// lo*hi) per tile pair, fp32 accumulation -- the fp32 1e-4 bar at bf16 MFMA rates.
+typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
+constexpr int BKP = BK + 8;  // X3 LDS row pitch (bf16): 80 B keeps 16-lane fragment reads conflict-free
+
+template <bool POOL2, bool X3>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
-  __shared__ float Ws[2][BK][BN + PADM];
-  __shared__ float Xs[2][BK][BM + PADM];
+  // fp32: Ws[2][BK][BN + PADM], Xs[2][BK][BM + PADM] (floats)
+  // X3:   Wh[2 buf][2 part][BN][BKP], Xh[2 buf][2 part][BM][BKP] (bf16)
+  constexpr int WS_BYTES = X3 ? 2 * 2 * BN * BKP * 2 : 2 * BK * (BN + PADM) * 4;
+  constexpr int XS_BYTES = X3 ? 2 * 2 * BM * BKP * 2 : 2 * BK * (BM + PADM) * 4;
+  __shared__ __attribute__((aligned(16))) char wsm[WS_BYTES];
+  __shared__ __attribute__((aligned(16))) char xsm[XS_BYTES];
+  float (*Ws)[BK][BN + PADM] = (float (*)[BK][BN + PADM])wsm;
+  float (*Xs)[BK][BM + PADM] = (float (*)[BK][BM + PADM])xsm;
+  __bf16 (*Wh)[2][BN][BKP] = (__bf16 (*)[2][BN][BKP])wsm;
+  __bf16 (*Xh)[2][BM][BKP] = (__bf16 (*)[2][BM][BKP])xsm;
   __shared__ int ktab[KTAB];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -64,6 +81,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
     }
 
   // X staging: thread owns pixel column mm = tid % 128 and rows kk = tid/128 + 2r
+  // (X3: the 16 consecutive rows 16 (tid/128) + r)
   const int mm = tid & (BM - 1);
   const int kq = tid >> 7;
   const int64_t mglob = m0 + mm;
@@ -105,7 +123,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
   auto load_slice = [&](int k0) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int k = k0 + kq + 2 * r;
+      const int k = k0 + (X3 ? kq * 16 + r : kq + 2 * r);
       xr[r] = (mvalid && k < a.K) ? a.in[xbase + koffset(k)] : 0.f;
     }
     const int n = n0 + wn_row;
@@ -121,10 +139,32 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
     }
   };
   auto store_slice = [&](int buf) {
+    if constexpr (X3) {
+      cbf16x8 xh[2], xl[2], whv, wlv;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) Xs[buf][kq + 2 * r][mm] = xr[r];
+      for (int r = 0; r < 16; ++r) {
+        const __bf16 h = (__bf16)xr[r];
+        xh[r >> 3][r & 7] = h;
+        xl[r >> 3][r & 7] = (__bf16)(xr[r] - (float)h);
+      }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Ws[buf][wk0 + j][wn_row] = wv[j];
+      for (int j = 0; j < 8; ++j) {
+        const __bf16 h = (__bf16)wv[j];
+        whv[j] = h;
+        wlv[j] = (__bf16)(wv[j] - (float)h);
+      }
+      *(cbf16x8*)&Xh[buf][0][mm][kq * 16] = xh[0];
+      *(cbf16x8*)&Xh[buf][0][mm][kq * 16 + 8] = xh[1];
+      *(cbf16x8*)&Xh[buf][1][mm][kq * 16] = xl[0];
+      *(cbf16x8*)&Xh[buf][1][mm][kq * 16 + 8] = xl[1];
+      *(cbf16x8*)&Wh[buf][0][wn_row][wk0] = whv;
+      *(cbf16x8*)&Wh[buf][1][wn_row][wk0] = wlv;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Xs[buf][kq + 2 * r][mm] = xr[r];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Ws[buf][wk0 + j][wn_row] = wv[j];
+    }
   };
 
   f32x4 acc[4][2];
@@ -141,19 +181,40 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
   for (int t = 0; t < nslices; ++t) {
     const int buf = t & 1;
     if (t + 1 < nslices) load_slice((t + 1) * BK);
+    if constexpr (X3) {
+      // one 32-deep k-step: lane (g, i16) holds k = 8g .. 8g+7 of row i16
+      const int kc = (lane >> 4) * 8, r16 = lane & 15;
+      cbf16x8 aw[2][4], bx[2][2];
 #pragma unroll
-    for (int ks = 0; ks < BK / 4; ++ks) {
-      const int kk = ks * 4 + (lane >> 4);
-      float av[4], bv[2];
+      for (int pt = 0; pt < 2; ++pt) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = Ws[buf][kk][i * 16 + (lane & 15)];
+        for (int i = 0; i < 4; ++i) aw[pt][i] = *(const cbf16x8*)&Wh[buf][pt][i * 16 + r16][kc];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bv[j] = Xs[buf][kk][wave * 32 + j * 16 + (lane & 15)];
+        for (int j = 0; j < 2; ++j) bx[pt][j] = *(const cbf16x8*)&Xh[buf][pt][wave * 32 + j * 16 + r16][kc];
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][i], bx[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][i], bx[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1][i], bx[0][j], acc[i][j], 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK / 4; ++ks) {
+        const int kk = ks * 4 + (lane >> 4);
+        float av[4], bv[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = Ws[buf][kk][i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = Xs[buf][kk][wave * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
     }
     if (t + 1 < nslices) store_slice(buf ^ 1);
     __syncthreads();
@@ -217,16 +278,20 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ 
   out[i] = m;
 }
 
-static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st) {
+static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st, bool x3 = false) {
   if (a.M <= 0 || a.N <= 0) return HONK_OK;
   const int64_t gm = cdiv(a.M, BM);
   if (gm > 0x7fffffff) return fail(HONK_ERR_ARG, "GEMM too large (M=%lld)", (long long)a.M);
   dim3 grid((unsigned)gm, (unsigned)cdiv(a.N, BN));
   TimedLaunch tl(st, 2.0 * (double)a.M * a.N * a.K);
-  if (pool2)
-    hipLaunchKernelGGL((conv_gemm_kernel<true>), grid, dim3(256), 0, st, a);
+  if (pool2 && x3)
+    hipLaunchKernelGGL((conv_gemm_kernel<true, true>), grid, dim3(256), 0, st, a);
+  else if (pool2)
+    hipLaunchKernelGGL((conv_gemm_kernel<true, false>), grid, dim3(256), 0, st, a);
+  else if (x3)
+    hipLaunchKernelGGL((conv_gemm_kernel<false, true>), grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((conv_gemm_kernel<false>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_gemm_kernel<false, false>), grid, dim3(256), 0, st, a);
   tl.done(st);
   HONK_LAUNCH_CHECK("conv_gemm_kernel");
   return HONK_OK;
@@ -234,7 +299,7 @@ static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st) {
 
 static int conv(const float* in, const float* w, const float* bias, float* out, int64_t batch, int cin,
                 int h, int wd, int cout, int kh, int kw, int sh, int sw, int relu, hipStream_t st,
-                bool pool2 = false) {
+                bool pool2 = false, bool x3 = false) {
   if (kh > h || kw > wd || sh < 1 || sw < 1 || cin < 1 || cout < 1)
     return fail(HONK_ERR_ARG, "bad conv geometry (cin=%d %dx%d k=%dx%d s=%dx%d)", cin, h, wd, kh, kw, sh, sw);
   GemmArgs a;
@@ -249,7 +314,7 @@ static int conv(const float* in, const float* w, const float* bias, float* out, 
   a.K = cin * kh * kw;
   a.relu = relu;
   if (pool2 && (a.PH < 1 || a.PW < 1)) return fail(HONK_ERR_ARG, "pool larger than conv output");
-  return launch_gemm(a, pool2, st);
+  return launch_gemm(a, pool2, st, x3);
 }
 
 // Linear with few outputs (n <= NB, e.g. cnn-trad-pool2's 26624 -> 4 output
@@ -323,7 +388,7 @@ __global__ __launch_bounds__(256) void linear_small_kernel(const float* __restri
 }
 
 static int linear(const float* x, const float* w, const float* b, float* y, int64_t m, int k, int n,
-                  int relu, hipStream_t st) {
+                  int relu, hipStream_t st, bool x3 = false) {
   if (n <= 16 && m > 0) {
     constexpr int CPB = 4;
     const unsigned blocks = (unsigned)cdiv(m, CPB);
@@ -336,7 +401,7 @@ static int linear(const float* x, const float* w, const float* b, float* y, int6
     HONK_LAUNCH_CHECK("linear_small_kernel");
     return HONK_OK;
   }
-  return conv(x, w, b, y, m, k, 1, 1, n, 1, 1, 1, 1, relu, st);
+  return conv(x, w, b, y, m, k, 1, 1, n, 1, 1, 1, 1, relu, st, false, x3);
 }
 
 static int maxpool(const float* in, float* out, int64_t planes, int h, int w, int kh, int kw, hipStream_t st) {
@@ -458,6 +523,9 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
   if (d->dnn2 && !d->dnn1) return fail(HONK_ERR_ARG, "dnn2 without dnn1");
   const size_t need = honk_cnn_workspace_bytes(d, batch);
   if (ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  if (d->precision != HONK_PREC_F32 && d->precision != HONK_PREC_BF16X3)
+    return fail(HONK_ERR_UNSUPPORTED, "cnn path precision %d (f32 or bf16x3)", d->precision);
+  const bool x3 = d->precision == HONK_PREC_BF16X3;
   hipStream_t st = (hipStream_t)stream;
   const int64_t chunk = chunk_clips(s, batch);
   float* A = (float*)workspace;
@@ -469,7 +537,7 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
     // conv1 + ReLU (model.py:187) -> A ; pool1 (:189) -> B (skip when 1x1)
     const bool fuse1 = d->p1_h == 2 && d->p1_w == 2;  // conv1 + ReLU + MaxPool2d(2,2) in one kernel
     rc = conv(xin, t[0], t[1], A, n, 1, d->height, d->width, d->c1_out, d->c1_kh, d->c1_kw, d->c1_sh, d->c1_sw, 1,
-              st, fuse1);
+              st, fuse1, x3);
     if (rc) return rc;
     const float* cur = A;
     float* other = B;
@@ -482,7 +550,7 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
     if (d->has_conv2) {  // model.py:190-193
       const bool fuse2 = d->p2_h == 2 && d->p2_w == 2;
       rc = conv(cur, t[2], t[3], other, n, d->c1_out, s.ph1, s.pw1, d->c2_out, d->c2_kh, d->c2_kw, d->c2_sh,
-                d->c2_sw, 1, st, fuse2);
+                d->c2_sw, 1, st, fuse2, x3);
       if (rc) return rc;
       const float* c2 = other;
       float* o2 = (float*)cur;
@@ -498,24 +566,24 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
     }
     int width = s.flat;  // flatten is free: NCHW (model.py:194)
     if (d->has_lin) {    // :195-196
-      rc = linear(cur, t[4], t[5], other, n, width, 32, 0, st);
+      rc = linear(cur, t[4], t[5], other, n, width, 32, 0, st, x3);
       if (rc) return rc;
       width = 32;
       float* tmp = other; other = (float*)cur; cur = tmp;
     }
     if (d->dnn1) {       // :197-201
-      rc = linear(cur, t[6], t[7], other, n, width, d->dnn1, d->dnn1_relu, st);
+      rc = linear(cur, t[6], t[7], other, n, width, d->dnn1, d->dnn1_relu, st, x3);
       if (rc) return rc;
       width = d->dnn1;
       float* tmp = other; other = (float*)cur; cur = tmp;
     }
     if (d->dnn2) {       // :202-204
-      rc = linear(cur, t[8], t[9], other, n, width, d->dnn2, 0, st);
+      rc = linear(cur, t[8], t[9], other, n, width, d->dnn2, 0, st, x3);
       if (rc) return rc;
       width = d->dnn2;
       float* tmp = other; other = (float*)cur; cur = tmp;
     }
-    rc = linear(cur, t[10], t[11], logits + c0 * d->n_labels, n, width, d->n_labels, 0, st);  // :205
+    rc = linear(cur, t[10], t[11], logits + c0 * d->n_labels, n, width, d->n_labels, 0, st, x3);  // :205
     if (rc) return rc;
   }
   return HONK_OK;

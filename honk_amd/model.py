@@ -314,6 +314,9 @@ class SpeechModel(SerializableModule):
             self.output.bias.data.zero_()
         self.dropout = nn.Dropout(dropout_prob)
         self._honk_desc = desc
+        # "f32": fp32 MFMA; "bf16x3": operands split into bf16 hi/lo pairs on the
+        # bf16 MFMA pipe (same 1e-4 logit bar; tests/test_gpu_cnn_x3.py)
+        self.honk_precision = "f32"
 
     # -- reference forward (CPU tensors / training mode): model.py:186-205 --
     def _torch_forward(self, x):
@@ -361,7 +364,9 @@ class SpeechModel(SerializableModule):
             if t is not None and (t.device != x.device or t.dtype != torch.float32):
                 raise RuntimeError(f"honk_amd: parameters must be float32 on {x.device}")
         ts = [t.detach().contiguous() if t is not None else None for t in ts]
-        desc = _native.CnnDesc(**d)
+        if self.honk_precision not in ("f32", "bf16x3"):
+            raise ValueError("SpeechModel.honk_precision must be 'f32' or 'bf16x3'")
+        desc = _native.CnnDesc(**d, precision=_native.PRECISIONS[self.honk_precision])
         B = x.shape[0]
         with torch.cuda.device(x.device):
             out = torch.empty(B, d["n_labels"], dtype=torch.float32, device=x.device)

@@ -80,6 +80,8 @@ typedef struct honk_cnn_desc {
   int32_t has_lin;                                        /* Linear(flat, 32), no ReLU */
   int32_t dnn1, dnn2;                                     /* 0 = absent              */
   int32_t dnn1_relu;                                      /* 1 unless tf_variant     */
+  int32_t precision;  /* HONK_PREC_F32 or HONK_PREC_BF16X3 (convs and >16-output Linears on the
+                         bf16 MFMA pipe with hi/lo-split operands; 1e-4 parity)  */
 } honk_cnn_desc;
 
 size_t honk_cnn_workspace_bytes(const honk_cnn_desc* d, int64_t batch);
