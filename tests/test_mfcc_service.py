@@ -87,3 +87,22 @@ def test_gpu_service_matches_cpu_service(tmp_path):
     lg, pg = gpu.label(wins[0])
     lc, pc = cpu.label(wins[0])
     assert lg == lc and abs(pg - pc) < 1e-4
+
+
+@pytest.mark.gpu
+def test_gpu_mfcc_mfma_matches_valu_path(monkeypatch):
+    """The MFMA power-spectrum kernel (default) against the direct-DFT VALU kernel
+    (HONK_MFCC_VALU=1) and the float64 oracle, on speech-like and silent clips."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ys = np.stack([_speechlike(s) for s in range(7)] + [np.zeros(16000, np.float32)])
+    ap = AudioPreprocessor()
+    fast = ap.compute_mfccs_batch(torch.from_numpy(ys).to(DEV)).cpu().numpy()
+    monkeypatch.setenv("HONK_MFCC_VALU", "1")
+    slow = ap.compute_mfccs_batch(torch.from_numpy(ys).to(DEV)).cpu().numpy()
+    assert np.isfinite(fast).all()
+    for i in range(len(ys)):
+        ref = mfcc_ref.mfcc(ys[i])
+        scale = max(np.abs(ref).max(), 1e-6)
+        np.testing.assert_allclose(fast[i], ref, atol=1e-3 * scale, rtol=0)
+        np.testing.assert_allclose(fast[i], slow[i], atol=1e-3 * scale, rtol=0)
