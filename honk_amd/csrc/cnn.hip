@@ -145,13 +145,21 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
       for (int r = 0; r < 16; ++r) {
         const __bf16 h = (__bf16)xr[r];
         xh[r >> 3][r & 7] = h;
+#ifdef HONK_CNN_ABLATE_SPLIT
+        xl[r >> 3][r & 7] = h;
+#else
         xl[r >> 3][r & 7] = (__bf16)(xr[r] - (float)h);
+#endif
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const __bf16 h = (__bf16)wv[j];
         whv[j] = h;
+#ifdef HONK_CNN_ABLATE_SPLIT
+        wlv[j] = h;
+#else
         wlv[j] = (__bf16)(wv[j] - (float)h);
+#endif
       }
       *(cbf16x8*)&Xh[buf][0][mm][kq * 16] = xh[0];
       *(cbf16x8*)&Xh[buf][0][mm][kq * 16 + 8] = xh[1];
