@@ -72,8 +72,15 @@ def cpu_baseline(cfg, seconds):
         orc.forward(params, cfg, x, acc=np.float32)
         n += per
     dt = time.perf_counter() - t0
+    model_name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model_name = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model_name)
+    except OSError:  # pragma: no cover
+        pass
     return {"value": n / dt, "unit": "clips/s", "cores": int(cores), "kind": "port",
-            "sample": f"{n} clips of {cfg_name(cfg)} in {dt:.1f} s (oracle/ref_numpy.py fp32, batches of {per})"}
+            "sample": f"{n} clips of {cfg_name(cfg)} in {dt:.1f} s (oracle/ref_numpy.py fp32, batches of {per})",
+            "cpu_model": model_name, "os_cpu_count": os.cpu_count()}
 
 
 def cfg_name(cfg):
