@@ -549,6 +549,7 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 }
 
 #include "res_bf16.inc"
+#include "res_bf16r.inc"
 
 // --------------------------------------------------------------------------- //
 // weight packing
@@ -733,6 +734,65 @@ static int dispatch_block16(const Plan& p, int SP, const Block16Args& a, hipStre
   return fail(HONK_ERR_UNSUPPORTED, "no bf16 block kernel for NT=%d MT=%d SP=%d", p.NT, p.MT, SP);
 }
 
+// Row-band kernel plan (res_bf16r.inc): same (NT, MT) as plan_block16; TH rows of
+// one dilation class per tile, limited by the tile's pixels and by the staging
+// image (TH + 2 rows); th = 0: not applicable (fall back to block16_kernel).
+// HONK_RES_ROWBAND=0 selects the per-dy-stage kernel for A/B runs.
+struct PlanR {
+  int NT, MT, TH;
+};
+static PlanR plan_block16r(const Layout& L, int SP) {
+  const Plan p = plan_block16(L, SP);
+  PlanR r{p.NT, p.MT, 0};
+  if (const char* e = getenv("HONK_RES_ROWBAND"))
+    if (atoi(e) == 0) return r;
+  if (SP == 1 && p.NT == 3) return r;  // (3,3,1): 3 x aoff spills at 2 waves/SIMD -> per-dy-stage kernel
+  const int MP = 16 * g16_nw(SP) * p.MT;
+  const int rpx = g16r_rpx(L.NT, MP / 128, SP);
+  int th = MP / L.W;
+  if (rpx / L.W - 2 < th) th = rpx / L.W - 2;
+  if (th < 1 || (th + 2) * L.W * L.CP * 2 * SP / 16 < 64) return r;
+  r.TH = th;
+  return r;
+}
+static int max_bands_per_clip(const Layout& L, int TH, int use_dilation) {
+  int best = 0;
+  for (int i = 1; i <= L.L; ++i) {
+    const int n = band_geo(L.H, use_dilation ? (1 << ((i - 1) / 3)) : 1, TH).nbc;
+    if (n > best) best = n;
+  }
+  return best;
+}
+
+template <int NT, int MT, int SP>
+static int launch_block16r(const Block16RArgs& a, hipStream_t st) {
+  using G = G16<NT, MT, SP>;
+  static_assert(G16R<NT, MT, SP>::LDS <= 160 * 1024, "LDS");
+  int grid = cu_count();
+  if (grid > a.ntiles) grid = a.ntiles;
+  const dim3 gd(grid), bd(G::NTHREADS);
+  const bool last = a.chsum != nullptr, res = a.res != nullptr;
+  if (last && res) hipLaunchKernelGGL((block16r_kernel<NT, MT, SP, true, true>), gd, bd, 0, st, a);
+  else if (last) hipLaunchKernelGGL((block16r_kernel<NT, MT, SP, true, false>), gd, bd, 0, st, a);
+  else if (res) hipLaunchKernelGGL((block16r_kernel<NT, MT, SP, false, true>), gd, bd, 0, st, a);
+  else hipLaunchKernelGGL((block16r_kernel<NT, MT, SP, false, false>), gd, bd, 0, st, a);
+  HONK_LAUNCH_CHECK("res block16r_kernel");
+  return HONK_OK;
+}
+
+static int dispatch_block16r(const PlanR& p, int SP, const Block16RArgs& a, hipStream_t st) {
+  static_assert(HONK_B16_NW == 8 && HONK_X3_NW == 8 && !HONK_X3_WREG, "row-band kernel: 8-wave build");
+  if (SP == 1) {
+    if (p.NT == 1 && p.MT == 4) return launch_block16r<1, 4, 1>(a, st);
+    if (p.NT == 2 && p.MT == 4) return launch_block16r<2, 4, 1>(a, st);
+  } else {
+    if (p.NT == 1 && p.MT == 4) return launch_block16r<1, 4, 2>(a, st);
+    if (p.NT == 2 && p.MT == 2) return launch_block16r<2, 2, 2>(a, st);
+    if (p.NT == 3 && p.MT == 1) return launch_block16r<3, 1, 2>(a, st);
+  }
+  return fail(HONK_ERR_UNSUPPORTED, "no row-band kernel for NT=%d MT=%d SP=%d", p.NT, p.MT, SP);
+}
+
 template <int NT, int MT>
 static int launch_block(const BlockArgs& a, hipStream_t st) {
   using G = Geo<NT, MT>;
@@ -789,9 +849,53 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
   __bf16* X = R + act;
   float* chsum = (float*)(R + 2 * act);
   const Plan p = plan_block16(L, SP);
+  const PlanR pr = plan_block16r(L, SP);
   const double layer_flop_per_clip = 2.0 * L.H * L.W * L.C * L.C * 9;
   if (L.L == 0) return fail(HONK_ERR_UNSUPPORTED, "bf16 path needs n_layers >= 1");
   int rc;
+  if (pr.TH > 0) {
+    // row-band kernel: tiles = (clip, dilation class, band of TH class rows)
+    int nbc_last = 0;
+    for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
+      const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
+      rc = (SP == 2) ? launch_conv0<__bf16, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+                     : launch_conv0<__bf16, false>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+      if (rc) return rc;
+      for (int i = 1; i <= L.L; ++i) {
+        const bool even = (i % 2) == 0;
+        Block16RArgs a;
+        a.in = even ? X : R;
+        a.res = even ? R : nullptr;
+        a.out = (i == L.L) ? nullptr : (even ? R : X);
+        a.bfrag = (const uint4*)(SP == 2 ? packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats
+                                         : packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
+        a.bias = packed + L.off_bias16 + (size_t)16 * L.CP * (i - 1);
+        a.chsum = (i == L.L) ? chsum : nullptr;
+        a.H = L.H;
+        a.W = L.W;
+        a.dil = d->use_dilation ? (1 << ((i - 1) / 3)) : 1;
+        a.TH = pr.TH;
+        const BandGeo bg = band_geo(L.H, a.dil, pr.TH);
+        a.nbc = bg.nbc;
+        a.rem = bg.rem;
+        a.nb1 = bg.nb1;
+        a.nb0 = bg.nb0;
+        if ((int64_t)n * a.nbc > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
+        a.ntiles = (int)(n * a.nbc);
+        if (i == L.L) nbc_last = a.nbc;
+        TimedLaunch tl(st, layer_flop_per_clip * (double)n);
+        rc = dispatch_block16r(pr, SP, a, st);
+        tl.done(st);
+        if (rc) return rc;
+      }
+      const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
+      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * g16_nw(SP), L.H * L.W, L.C, L.CP, L.NL,
+                         bn_last, bn_last + L.CP);
+      HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16 row-band)");
+    }
+    return HONK_OK;
+  }
   for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
     const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
     if ((int64_t)n * p.nbands > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
@@ -868,7 +972,13 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   if (L.prec != HONK_PREC_F32) {
     const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;
     const Plan p = plan_block16(L, SP);
-    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * p.nbands * g16_nw(SP) * L.CP * sizeof(float);
+    const PlanR pr = plan_block16r(L, SP);
+    int nb = p.nbands;
+    if (pr.TH > 0) {
+      const int nr = max_bands_per_clip(L, pr.TH, d->use_dilation);
+      if (nr > nb) nb = nr;
+    }
+    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * nb * g16_nw(SP) * L.CP * sizeof(float);
   }
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
