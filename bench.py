@@ -199,10 +199,12 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model):
     per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1)) / L
     bw = per_clip * clips / avg_s / 1e9 if nl else None
     mf = (kfl * (3 if sp == 2 else 1) / max(nl, 1)) / avg_s / 1e12 if nl else None
-    return {"bound": "hbm", "kernel": f"honk::res::block16_kernel<..., SP={sp}> (dilated 3x3 conv, bf16 MFMA)",
+    # 45-map bf16 runs the per-dy-stage kernel; bf16x3 and narrow maps the row-band kernel
+    fam = "block16_kernel" if (sp == 1 and CP == 48) else "block16r_kernel"
+    return {"bound": "hbm", "kernel": f"honk::res::{fam}<..., SP={sp}> (dilated 3x3 conv, bf16 MFMA)",
             "achieved": round(bw, 1) if bw else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(bw / HBM_PEAK_GBS, 4) if bw else None,
-            "traffic": load_traffic(f"block16_kernel_sp{sp}", clips, model),
+            "traffic": load_traffic(f"{fam}_sp{sp}", clips, model),
             "launches": nl, "avg_launch_ms": round(kms / max(nl, 1), 4),
             "algorithmic_bytes_per_launch": per_clip * clips,
             "mfma": {"executed_bf16_tflops": round(mf, 2) if mf else None, "peak": BF16_MFMA_PEAK_TFLOPS,
