@@ -605,7 +605,7 @@ struct Layout {
   int C, CP, NT, L, NL, prec, KS16;
   int Hin, Win, H, W, ph, pw;
   size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, off_frag16, frag16_floats,
-      off_fragx3, fragx3_floats, off_bias16, total;
+      off_fragx3, fragx3_floats, off_fragr16, off_fragrx3, off_bias16, total;
 };
 
 static size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
@@ -646,8 +646,12 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   L->frag16_floats = (size_t)g16_frag_bytes(L->NT, 1) / 4;
   L->off_fragx3 = L->off_frag16 + L->frag16_floats * L->L;
   L->fragx3_floats = (size_t)g16_frag_bytes(L->NT, 2) / 4;
+  // the same fragments in the row-band kernel's k order (k-steps run across the
+  // three dy rows: G16R::xfrag; same byte count)
+  L->off_fragr16 = L->off_fragx3 + L->fragx3_floats * L->L;
+  L->off_fragrx3 = L->off_fragr16 + L->frag16_floats * L->L;
   // folded input-BN bias [L][16 classes][CP] for the bf16 kernel
-  L->off_bias16 = L->off_fragx3 + L->fragx3_floats * L->L;
+  L->off_bias16 = L->off_fragrx3 + L->fragx3_floats * L->L;
   L->total = L->off_bias16 + (size_t)16 * L->CP * L->L;
   L->prec = d->precision;
   if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16 && L->prec != HONK_PREC_BF16X3)
@@ -867,8 +871,8 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         a.in = even ? X : R;
         a.res = even ? R : nullptr;
         a.out = (i == L.L) ? nullptr : (even ? R : X);
-        a.bfrag = (const uint4*)(SP == 2 ? packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats
-                                         : packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
+        a.bfrag = (const uint4*)(SP == 2 ? packed + L.off_fragrx3 + (size_t)(i - 1) * L.fragx3_floats
+                                         : packed + L.off_fragr16 + (size_t)(i - 1) * L.frag16_floats);
         a.bias = packed + L.off_bias16 + (size_t)16 * L.CP * (i - 1);
         a.chsum = (i == L.L) ? chsum : nullptr;
         a.H = L.H;
@@ -1009,9 +1013,13 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
     const float* in_bn = (i > 0) ? packed + L.off_bn + (size_t)2 * L.CP * (i - 1) : nullptr;
     const int n16 = 3 * L.KS16 * L.NT * 64 * 8;
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
-                       (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16, 1);
+                       (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16, 1, 0);
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
-                       (__bf16*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, L.KS16, 2);
+                       (__bf16*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, L.KS16, 2, 0);
+    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
+                       (__bf16*)(packed + L.off_fragr16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16, 1, 1);
+    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
+                       (__bf16*)(packed + L.off_fragrx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, L.KS16, 2, 1);
     HONK_LAUNCH_CHECK("pack_block16");
     hipLaunchKernelGGL(pack_bias16_kernel, dim3(cdiv(16 * L.CP, 256)), dim3(256), 0, st, t[1 + i],
                        in_bn ? in_bn + L.CP : nullptr, packed + L.off_bias16 + (size_t)16 * L.CP * i, L.C, L.CP);
