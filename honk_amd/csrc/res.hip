@@ -785,14 +785,15 @@ static int launch_block16r(const Block16RArgs& a, hipStream_t st) {
 }
 
 static int dispatch_block16r(const PlanR& p, int SP, const Block16RArgs& a, hipStream_t st) {
-  static_assert(HONK_B16_NW == 8 && HONK_X3_NW == 8 && !HONK_X3_WREG, "row-band kernel: 8-wave build");
+  static_assert(HONK_B16_NW == 8 && !HONK_X3_WREG, "row-band kernel: 8-wave bf16 build, no WREG");
+  constexpr int X = 8 / HONK_X3_NW;  // m-tiles per wave scale with 8 / waves per workgroup
   if (SP == 1) {
     if (p.NT == 1 && p.MT == 4) return launch_block16r<1, 4, 1>(a, st);
     if (p.NT == 2 && p.MT == 4) return launch_block16r<2, 4, 1>(a, st);
   } else {
-    if (p.NT == 1 && p.MT == 4) return launch_block16r<1, 4, 2>(a, st);
-    if (p.NT == 2 && p.MT == 2) return launch_block16r<2, 2, 2>(a, st);
-    if (p.NT == 3 && p.MT == 1) return launch_block16r<3, 1, 2>(a, st);
+    if (p.NT == 1 && p.MT == 4 * X) return launch_block16r<1, 4 * X, 2>(a, st);
+    if (p.NT == 2 && p.MT == 2 * X) return launch_block16r<2, 2 * X, 2>(a, st);
+    if (p.NT == 3 && p.MT == 1 * X) return launch_block16r<3, 1 * X, 2>(a, st);
   }
   return fail(HONK_ERR_UNSUPPORTED, "no row-band kernel for NT=%d MT=%d SP=%d", p.NT, p.MT, SP);
 }
