@@ -54,22 +54,25 @@ def parse():
 
 
 def cpu_baseline(cfg, seconds):
-    """Oracle (numpy fp32 im2col+BLAS restatement) on the host cores: bounded sample."""
+    """The reference's CPU path restated (oracle/ref_torch.py: stock torch fp32 eval
+    forward, what utils/train.py --no_cuda runs) on the host cores: bounded sample.
+    Threads = the box's CPU share (16 on the GPU pool; os.cpu_count() shows the
+    whole machine there), batches as SURVEY.md §8(d): 64 clips for res15, else 256."""
+    import torch
     from oracle import ref_numpy as orc
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:  # pragma: no cover
-        cores = os.cpu_count()
-    params = orc.make_params(cfg, 0)
+    from oracle import ref_torch
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    params = ref_torch.tensors(orc.make_params(cfg, 0))
     rng = np.random.Generator(np.random.PCG64(1))
-    per = 4
-    x = rng.standard_normal((per, 101, 40)).astype(np.float32)
-    orc.forward(params, cfg, x[:1], acc=np.float32)  # warm-up
+    per = 64 if int(cfg.get("n_layers", 0)) > 8 else 256
+    x = torch.from_numpy(rng.standard_normal((per, 101, 40)).astype(np.float32))
+    ref_torch.forward(params, cfg, x[:2])  # warm-up
+    ref_torch.forward(params, cfg, x)
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        orc.forward(params, cfg, x, acc=np.float32)
+        ref_torch.forward(params, cfg, x)
         n += per
     dt = time.perf_counter() - t0
     model_name = "unknown"
@@ -79,7 +82,8 @@ def cpu_baseline(cfg, seconds):
     except OSError:  # pragma: no cover
         pass
     return {"value": n / dt, "unit": "clips/s", "cores": int(cores), "kind": "port",
-            "sample": f"{n} clips of {cfg_name(cfg)} in {dt:.1f} s (oracle/ref_numpy.py fp32, batches of {per})",
+            "sample": f"{n} clips of {cfg_name(cfg)} in {dt:.1f} s (oracle/ref_torch.py: torch {torch.__version__} "
+                      f"CPU fp32 eval forward, batches of {per}, {cores} threads)",
             "cpu_model": model_name, "os_cpu_count": os.cpu_count()}
 
 

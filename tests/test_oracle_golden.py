@@ -44,3 +44,12 @@ def test_flops_per_clip_matches_survey():
     assert orc.flops_per_clip(c["cnn-trad-pool2"]) == 2 * 95_973_376
     cfg = dict(c["cnn-one-fstride4"], n_labels=12)
     assert orc.flops_per_clip(cfg) == 2 * 1_428_176
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_torch_oracle_matches_reference_logits(name):
+    # oracle/ref_torch.py: the fp32 torch-CPU restatement timed as bench.py's cpu_baseline
+    from oracle import ref_torch
+    cfg, params, x, logits, meta = load_fixture(name)
+    out = ref_torch.forward(params, cfg, x).numpy()
+    np.testing.assert_allclose(out, logits, atol=1e-5, rtol=1e-4)
