@@ -33,6 +33,7 @@ struct GemmArgs {
   int Cin, H, W, KH, KW, SH, SW, OH, OW;
   int PH, PW;        // pooled output dims (pool2 fused)
   int relu;
+  int nhwc_x3;       // POOL2 only: store [B][PH][PW][hi N | lo N] bf16 (conv2x3_kernel's input) instead of NCHW fp32
 };
 
 // D[n][m] = act(bias[n] + sum_k W[n][k] * X[k][m]) on v_mfma_f32_16x16x4_f32.
@@ -51,6 +52,7 @@ struct GemmArgs {
 // slice is ONE v_mfma_f32_16x16x32_bf16 step of 3 products (hi*hi + hi*lo +
 // lo*hi) per tile pair, fp32 accumulation -- the fp32 1e-4 bar at bf16 MFMA rates.
 typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4c __attribute__((ext_vector_type(4)));
 constexpr int BKP = BK + 8;  // X3 LDS row pitch (bf16): 80 B keeps 16-lane fragment reads conflict-free
 
 template <bool POOL2, bool X3>
@@ -249,6 +251,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      float pooled[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + i * 16 + (lane >> 4) * 4 + r;
@@ -257,10 +260,25 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
         if (POOL2) {  // max over the 2x2 window = lanes l, l^1, l^2, l^3 (same n)
           v = fmaxf(v, __shfl_xor(v, 1));
           v = fmaxf(v, __shfl_xor(v, 2));
-          if ((lane & 3) == 0 && mok && n < a.N) a.out[obase + (int64_t)n * plane] = v;
+          if (a.nhwc_x3) pooled[r] = v;
+          else if ((lane & 3) == 0 && mok && n < a.N) a.out[obase + (int64_t)n * plane] = v;
         } else if (mok && n < a.N) {
           a.out[obase + (int64_t)n * plane] = v;
         }
+      }
+      if (POOL2 && a.nhwc_x3 && (lane & 3) == 0 && mok) {
+        // the lane's 4 consecutive channels of its pooled pixel, split into bf16
+        // (hi, lo) runs of the [hi N | lo N] pixel (N == 64: host-checked)
+        const int n = n0 + i * 16 + (lane >> 4) * 4;
+        bf16x4c hv, lv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          hv[r] = (__bf16)pooled[r];
+          lv[r] = (__bf16)(pooled[r] - (float)hv[r]);
+        }
+        __bf16* px = (__bf16*)a.out + (m >> 2) * (int64_t)(2 * a.N);
+        *(bf16x4c*)(px + n) = hv;
+        *(bf16x4c*)(px + a.N + n) = lv;
       }
     }
   }
@@ -286,6 +304,343 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ 
   out[i] = m;
 }
 
+
+// ---------------------------------------------------------------------------- //
+// conv2 of cnn-trad-pool2 (64 -> <= 64 channels, stride 1, no pool after it) in
+// bf16x3 on an NHWC hi/lo input: the whole clip is one tile.
+//
+// The input (conv1 + ReLU + MaxPool2d(2,2) output, written by conv_gemm_kernel's
+// nhwc_x3 epilogue as [B][PH][PW][hi 64 | lo 64] bf16) is staged per clip in two
+// 32-channel halves: one LDS image of PH*PW pixels x 128 B ([hi 32 | lo 32]) per
+// half, filled by LDS-DMA, its 16-B chunks XOR-swizzled by pixel (chunk c of
+// pixel P at slot P*8 + (c ^ (P & 7))) so a fragment read spreads over the banks.
+// Implicit GEMM, weights as the MFMA A operand (16 out channels x 32 k), the
+// image as B (32 k x 16 output pixels): k-step s = (half, tap kh*KW + kw) over
+// the half's 32 channels, lane group g holding channels 8g .. 8g+7.
+// 4 waves (one per SIMD): wave = (n-group: out tiles 2ng, 2ng+1) x (m-group: MT
+// consecutive 16-pixel tiles of the clip's OH*OW outputs).  Each k-step reads
+// the wave's MT A fragment pairs from LDS and its 4 weight fragments (hi, lo of
+// 2 out tiles, pre-split by pack_conv2x3_kernel, L2-resident) from global, both
+// one k-step ahead, and runs 6 MT MFMAs (hi*hi + hi*lo + lo*hi).
+// Epilogue: bias + ReLU, NCHW fp32 stores (flatten order of model.py:194).
+// ---------------------------------------------------------------------------- //
+constexpr int C2X3_IMG = 96 * 1024;  // LDS bytes of one half image (PH*PW*128 <= this)
+
+struct Conv2X3Args {
+  const __bf16* in;    // [B][PH][PW][hi 64 | lo 64]
+  const uint4* wfrag;  // [2*ntap k-steps][4 out tiles][2 parts][64 lanes] x 16 B
+  const float* bias;   // [N]
+  float* out;          // [B][N][OH][OW]
+  int B, PH, PW, KW, ntap, OH, OW, N;
+};
+
+template <int MT>
+__global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
+  __shared__ __attribute__((aligned(16))) char img[C2X3_IMG];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ng = wave & 1, mg = wave >> 1;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int npx = a.PH * a.PW;
+  const int ohw = a.OH * a.OW;
+  const int chunks = npx * 8;
+  const int pieces = (chunks + 63) / 64;
+  const int clip_bytes = npx * 256;
+
+  // per m-tile: the lane's output pixel -> its input pixel at tap (0, 0)
+  int P0[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int p = (mg * MT + m) * 16 + i16;
+    const int oh = p / a.OW, ow = p - oh * a.OW;
+    P0[m] = p < ohw ? oh * a.PW + ow : 0;
+  }
+  const uint4* wl = a.wfrag + ng * 2 * 2 * 64 + lane;  // (s, nt = 2 ng + j, part) -> wl[(s*4 + j)*... ]
+
+  typedef uint4 AFr[MT][2];
+  typedef uint4 WFr[2][2];
+  auto loadA = [&](AFr& A, int delta) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int P = P0[m] + delta;
+      const int ad = ((P << 3) + (g ^ (P & 7))) << 4;
+      A[m][0] = *(const uint4*)(img + ad);
+      A[m][1] = *(const uint4*)(img + (ad ^ 64));
+    }
+  };
+  auto loadW = [&](WFr& Wr, int s) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) Wr[j][pt] = wl[((s * 4 + j) * 2 + pt) * 64];
+  };
+  f32x4 acc[MT][2];
+  auto mma = [&](const AFr& A, const WFr& Wr) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, Wr[j][t == 2 ? 1 : 0]),
+                                                              __builtin_bit_cast(cbf16x8, A[m][t == 1 ? 1 : 0]),
+                                                              acc[m][j], 0, 0, 0);
+  };
+  auto delta = [&](int t) {
+    const int kh = t / a.KW;
+    return kh * a.PW + (t - kh * a.KW);
+  };
+
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)a.in + (size_t)b * clip_bytes), (short)0, clip_bytes, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();  // every wave is done reading the previous image
+      for (int pc = wave; pc < pieces; pc += 4) {
+        const int st = __builtin_amdgcn_readfirstlane(min(pc * 64, chunks - 64));
+        const int L = st + lane;
+        const int P = L >> 3, c = (L & 7) ^ (P & 7);
+        const unsigned voff = (unsigned)(P * 256 + (c >> 2) * 128 + h * 64 + (c & 3) * 16);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + st * 16), 16,
+                                                 voff, 0, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces landed
+      __syncthreads();                     // ... and every wave's
+      const int s0 = h * a.ntap;
+      AFr A0, A1;
+      WFr W0, W1;
+      loadW(W0, s0);
+      loadA(A0, 0);
+      for (int t = 0; t < a.ntap; t += 2) {  // ntap even (host-checked)
+        loadW(W1, s0 + t + 1);
+        loadA(A1, delta(t + 1));
+        mma(A0, W0);
+        if (t + 2 < a.ntap) {
+          loadW(W0, s0 + t + 2);
+          loadA(A0, delta(t + 2));
+        }
+        mma(A1, W1);
+      }
+    }
+    // epilogue: lane (g, i16) holds out channels (2 ng + j) 16 + 4 g + r of pixel p
+    float* ob = a.out + (size_t)b * a.N * ohw;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int p = (mg * MT + m) * 16 + i16;
+      if (p < ohw) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = (2 * ng + j) * 16 + 4 * g + r;
+            if (n < a.N) ob[(size_t)n * ohw + p] = fmaxf(acc[m][j][r] + a.bias[n], 0.f);
+          }
+      }
+    }
+  }
+}
+
+// conv2 weights [N][64][KH][KW] fp32 -> conv2x3_kernel's fragments: k-step
+// s = half * ntap + tap, out tile nt, part (hi, lo), lane (g, i16):
+// 8 bf16 of W[16 nt + i16][32 half + 8 g + j][tap] (zero past N)
+__global__ void pack_conv2x3_kernel(const float* __restrict__ w, __bf16* __restrict__ frag, int N, int ntap) {
+  const int total = 2 * ntap * 4 * 2 * 64 * 8;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int r = i;
+  const int j = r & 7; r >>= 3;
+  const int lane = r & 63; r >>= 6;
+  const int pt = r & 1; r >>= 1;
+  const int nt = r & 3; r >>= 2;
+  const int s = r;
+  const int h = s / ntap, t = s - h * ntap;
+  const int co = nt * 16 + (lane & 15);
+  const int ci = 32 * h + 8 * (lane >> 4) + j;
+  const float v = co < N ? w[((size_t)co * 64 + ci) * ntap + t] : 0.f;
+  const __bf16 hi = (__bf16)v;
+  frag[i] = pt == 0 ? hi : (__bf16)(v - (float)hi);
+}
+
+
+// ---------------------------------------------------------------------------- //
+// conv1 + ReLU + MaxPool2d(2,2) of cnn-trad-pool2 (1 -> 64 channels, 20 x 8
+// filter, stride 1) in bf16x3, writing conv2x3_kernel's NHWC hi/lo input.
+// One clip per tile, 8 waves = 2 n-groups (out tiles 2ng, 2ng+1) x 4 m-groups.
+//   K = 160 = 5 k-steps: lane group g of k-step s holds kh = 4s + g, kw = 0..7,
+//   i.e. 8 consecutive input pixels of one row.  The clip is staged in LDS as a
+//   "shifted-row" image: entry (r, c) = x[r][c .. c+7] as 8 bf16, hi and lo in
+//   separate planes, c = 0 .. 31 (the pooled output's columns), entry slot
+//   r*32 + ((c + 8 r) & 31) (16-B entries: conflict-free fragment reads), so an
+//   A fragment is ONE aligned 16-B read and k-step s adds a fixed 2 KiB offset.
+//   Weights: the wave's 2 out tiles x 5 k-steps x (hi, lo) fragments live in
+//   VGPRs for the whole launch (W[co][kh][0..7] is 8 contiguous floats).
+//   M = pooled members (ph, pw, 2x2 member) so the 4 members of a window sit in
+//   lanes l .. l^3 of one MFMA column group: bias, ReLU, 2 lane-swap maxes, then
+//   the lane with member 0 stores 4 channels' hi and lo runs (8 B each).
+// ---------------------------------------------------------------------------- //
+constexpr int C1X3_KH = 20, C1X3_KW = 8, C1X3_COLS = 32, C1X3_HMAX = 101;
+constexpr int C1X3_PLANE = C1X3_HMAX * C1X3_COLS * 16;  // bytes of one (hi or lo) plane
+
+struct Conv1X3Args {
+  const float* x;     // [B][H][W]
+  const float* w;     // [64][1][20][8]
+  const float* bias;  // [64]
+  __bf16* out;        // [B][PH][PW][hi 64 | lo 64]
+  int B, H, W, PH, PW;
+};
+
+__global__ __launch_bounds__(512, 1) void conv1x3_kernel(Conv1X3Args a) {
+  __shared__ __attribute__((aligned(16))) char img[2 * C1X3_PLANE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ng = wave & 1, mg = wave >> 1;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int nmt = a.PH * a.PW / 4;  // 16-row m-tiles of pooled members (PH*PW % 4 == 0: host-checked)
+  const int clip_floats = a.H * a.W;
+  const int entries = a.H * C1X3_COLS;
+
+  // weight fragments in registers: [k-step][out tile j][part]
+  uint4 wf[5][2][2];
+#pragma unroll
+  for (int s = 0; s < 5; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = (2 * ng + j) * 16 + i16;
+      const float* src = a.w + ((size_t)co * C1X3_KH + 4 * s + g) * C1X3_KW;
+      const f32x4 u = *(const f32x4*)src, v = *(const f32x4*)(src + 4);
+      cbf16x8 h, l;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = e < 4 ? u[e] : v[e - 4];
+        h[e] = (__bf16)f;
+        l[e] = (__bf16)(f - (float)h[e]);
+      }
+      wf[s][j][0] = __builtin_bit_cast(uint4, h);
+      wf[s][j][1] = __builtin_bit_cast(uint4, l);
+    }
+  float bias[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[j][r] = a.bias[(2 * ng + j) * 16 + 4 * g + r];
+
+  // the lane's A-fragment byte offset (hi plane, k-step 0) for m-tile mt
+  auto aoff = [&](int mt) {
+    const int q = 4 * mt + (i16 >> 2), mem = i16 & 3;
+    const int ph = q / a.PW, pw = q - ph * a.PW;
+    const int r = 2 * ph + (mem >> 1) + g, c = 2 * pw + (mem & 1);
+    return (r * C1X3_COLS + ((c + 8 * r) & (C1X3_COLS - 1))) * 16;
+  };
+  typedef uint4 AFr[5][2];
+  auto loadA = [&](AFr& A, int off) {
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      A[s][0] = *(const uint4*)(img + off + s * 4 * C1X3_COLS * 16);
+      A[s][1] = *(const uint4*)(img + C1X3_PLANE + off + s * 4 * C1X3_COLS * 16);
+    }
+  };
+  auto tile = [&](const AFr& A, int mt, __bf16* ob) {
+    f32x4 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = f32x4{bias[j][0], bias[j][1], bias[j][2], bias[j][3]};
+#pragma unroll
+    for (int s = 0; s < 5; ++s)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, wf[s][j][t == 2 ? 1 : 0]),
+                                                           __builtin_bit_cast(cbf16x8, A[s][t == 1 ? 1 : 0]),
+                                                           acc[j], 0, 0, 0);
+    const int q = 4 * mt + (i16 >> 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf16x4c hv, lv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = fmaxf(acc[j][r], 0.f);
+        v = fmaxf(v, __shfl_xor(v, 1));
+        v = fmaxf(v, __shfl_xor(v, 2));
+        hv[r] = (__bf16)v;
+        lv[r] = (__bf16)(v - (float)hv[r]);
+      }
+      if ((i16 & 3) == 0) {
+        __bf16* px = ob + (size_t)q * 128 + (2 * ng + j) * 16 + 4 * g;
+        *(bf16x4c*)px = hv;
+        *(bf16x4c*)(px + 64) = lv;
+      }
+    }
+  };
+
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.x + (size_t)b * clip_floats), (short)0, clip_floats * 4, 0x00020000);
+    __syncthreads();  // every wave is done with the previous clip's image
+    for (int e = tid; e < entries; e += 512) {
+      const int r = e / C1X3_COLS, c = e - r * C1X3_COLS;
+      const int o = (r * a.W + c) * 4;
+      const f32x4 u = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+      const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, 0, 0));
+      cbf16x8 h, l;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float f = k < 4 ? u[k] : v[k - 4];
+        h[k] = (__bf16)f;
+        l[k] = (__bf16)(f - (float)h[k]);
+      }
+      const int slot = (r * C1X3_COLS + ((c + 8 * r) & (C1X3_COLS - 1))) * 16;
+      *(cbf16x8*)(img + slot) = h;
+      *(cbf16x8*)(img + C1X3_PLANE + slot) = l;
+    }
+    __syncthreads();
+    __bf16* ob = a.out + (size_t)b * a.PH * a.PW * 128;
+    AFr A0, A1;
+    int mt = mg;
+    if (mt < nmt) loadA(A0, aoff(mt));
+    while (mt < nmt) {
+      const int m1 = mt + 4;
+      if (m1 < nmt) loadA(A1, aoff(m1));
+      tile(A0, mt, ob);
+      if (m1 >= nmt) break;
+      const int m2 = m1 + 4;
+      if (m2 < nmt) loadA(A0, aoff(m2));
+      tile(A1, m1, ob);
+      mt = m2;
+    }
+  }
+}
+
+// conv1 on the fast path: bf16x3 with conv2x3 following, trad-pool2's conv1
+// geometry (20 x 8 filter, stride 1, 64 maps, 2x2 pool, 32 pooled-window columns)
+static bool conv1x3_applies(const honk_cnn_desc* d, int oh1, int ph1, int pw1) {
+  if (const char* e = getenv("HONK_CNN_C1X3"))
+    if (atoi(e) == 0) return false;
+  return d->c1_kh == C1X3_KH && d->c1_kw == C1X3_KW && d->c1_sh == 1 && d->c1_sw == 1 && d->c1_out == 64 &&
+         2 * pw1 == C1X3_COLS && d->width >= C1X3_COLS + C1X3_KW - 1 && d->height <= C1X3_HMAX &&
+         (ph1 * pw1) % 4 == 0 && oh1 >= 2 * ph1;
+}
+
+// cnn-trad-pool2-class conv2 on the fast path: bf16x3, conv1 pooled 2x2 with 64
+// maps (its GEMM writes the NHWC split input), conv2 64 -> <= 64, stride 1, no
+// pool after it, an even tap count, a half image within C2X3_IMG and OH*OW
+// within the instantiated 2 * 13 m-tiles
+constexpr int C2X3_MT = 13;
+static bool conv2x3_applies(const honk_cnn_desc* d, int ph1, int pw1, int oh2, int ow2) {
+  if (d->precision != HONK_PREC_BF16X3 || !d->has_conv2) return false;
+  if (const char* e = getenv("HONK_CNN_C2X3"))
+    if (atoi(e) == 0) return false;
+  return d->p1_h == 2 && d->p1_w == 2 && d->c1_out == 64 && d->c2_out <= 64 && d->c2_sh == 1 && d->c2_sw == 1 &&
+         d->p2_h == 1 && d->p2_w == 1 && (d->c2_kh * d->c2_kw) % 2 == 0 && ph1 * pw1 * 128 <= C2X3_IMG &&
+         oh2 * ow2 > 16 * C2X3_MT && oh2 * ow2 <= 32 * C2X3_MT;
+}
+static size_t conv2x3_frag_bytes(const honk_cnn_desc* d) { return (size_t)2 * d->c2_kh * d->c2_kw * 4 * 2 * 64 * 16; }
+
 static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st, bool x3 = false) {
   if (a.M <= 0 || a.N <= 0) return HONK_OK;
   const int64_t gm = cdiv(a.M, BM);
@@ -307,7 +662,7 @@ static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st, bool x3 = 
 
 static int conv(const float* in, const float* w, const float* bias, float* out, int64_t batch, int cin,
                 int h, int wd, int cout, int kh, int kw, int sh, int sw, int relu, hipStream_t st,
-                bool pool2 = false, bool x3 = false) {
+                bool pool2 = false, bool x3 = false, bool nhwc_x3 = false) {
   if (kh > h || kw > wd || sh < 1 || sw < 1 || cin < 1 || cout < 1)
     return fail(HONK_ERR_ARG, "bad conv geometry (cin=%d %dx%d k=%dx%d s=%dx%d)", cin, h, wd, kh, kw, sh, sw);
   GemmArgs a;
@@ -321,6 +676,7 @@ static int conv(const float* in, const float* w, const float* bias, float* out, 
   a.N = cout;
   a.K = cin * kh * kw;
   a.relu = relu;
+  a.nhwc_x3 = nhwc_x3 ? 1 : 0;
   if (pool2 && (a.PH < 1 || a.PW < 1)) return fail(HONK_ERR_ARG, "pool larger than conv output");
   return launch_gemm(a, pool2, st, x3);
 }
@@ -512,7 +868,9 @@ int honk_linear_f32(const float* x, const float* w, const float* b, float* y, in
 size_t honk_cnn_workspace_bytes(const honk_cnn_desc* d, int64_t batch) {
   Shapes s;
   if (shapes(d, &s) != HONK_OK || batch < 1) return 0;
-  return (size_t)2 * chunk_clips(s, batch) * per_clip_floats(s) * sizeof(float);
+  size_t b = (size_t)2 * chunk_clips(s, batch) * per_clip_floats(s) * sizeof(float);
+  if (conv2x3_applies(d, s.ph1, s.pw1, s.oh2, s.ow2)) b += conv2x3_frag_bytes(d);  // packed conv2 fragments
+  return b;
 }
 
 int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float* x, float* logits, int64_t batch,
@@ -538,15 +896,43 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
   const int64_t chunk = chunk_clips(s, batch);
   float* A = (float*)workspace;
   float* B = A + chunk * per_clip_floats(s);
+  const bool c2x3 = conv2x3_applies(d, s.ph1, s.pw1, s.oh2, s.ow2);
+  uint4* c2frag = (uint4*)(B + chunk * per_clip_floats(s));
+  if (c2x3) {  // conv2 weights -> hi/lo fragments (one small launch per call)
+    const int ntap = d->c2_kh * d->c2_kw;
+    const int total = 2 * ntap * 4 * 2 * 64 * 8;
+    hipLaunchKernelGGL(pack_conv2x3_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, t[2],
+                       (__bf16*)c2frag, d->c2_out, ntap);
+    HONK_LAUNCH_CHECK("pack_conv2x3_kernel");
+  }
 
   for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
     const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
     const float* xin = x + c0 * d->height * d->width;
     // conv1 + ReLU (model.py:187) -> A ; pool1 (:189) -> B (skip when 1x1)
     const bool fuse1 = d->p1_h == 2 && d->p1_w == 2;  // conv1 + ReLU + MaxPool2d(2,2) in one kernel
-    rc = conv(xin, t[0], t[1], A, n, 1, d->height, d->width, d->c1_out, d->c1_kh, d->c1_kw, d->c1_sh, d->c1_sw, 1,
-              st, fuse1, x3);
-    if (rc) return rc;
+    if (c2x3 && conv1x3_applies(d, s.oh1, s.ph1, s.pw1)) {
+      Conv1X3Args c;
+      c.x = xin;
+      c.w = t[0];
+      c.bias = t[1];
+      c.out = (__bf16*)A;
+      c.B = (int)n;
+      c.H = d->height;
+      c.W = d->width;
+      c.PH = s.ph1;
+      c.PW = s.pw1;
+      if (n > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
+      const unsigned grid = (unsigned)(n < cu_count() ? n : cu_count());
+      TimedLaunch tl(st, 2.0 * (double)n * s.ph1 * s.pw1 * 4 * 64 * C1X3_KH * C1X3_KW);
+      hipLaunchKernelGGL(conv1x3_kernel, dim3(grid), dim3(512), 0, st, c);
+      tl.done(st);
+      HONK_LAUNCH_CHECK("conv1x3_kernel");
+    } else {
+      rc = conv(xin, t[0], t[1], A, n, 1, d->height, d->width, d->c1_out, d->c1_kh, d->c1_kw, d->c1_sh, d->c1_sw, 1,
+                st, fuse1, x3, c2x3);
+      if (rc) return rc;
+    }
     const float* cur = A;
     float* other = B;
     if (!fuse1 && d->p1_h * d->p1_w > 1) {
@@ -555,7 +941,29 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
       cur = B;
       other = A;
     }
-    if (d->has_conv2) {  // model.py:190-193
+    if (c2x3) {  // model.py:190-193 on the fast path (pool2 is 1x1)
+      Conv2X3Args c;
+      c.in = (const __bf16*)A;
+      c.wfrag = c2frag;
+      c.bias = t[3];
+      c.out = B;
+      c.B = (int)n;
+      c.PH = s.ph1;
+      c.PW = s.pw1;
+      c.KW = d->c2_kw;
+      c.ntap = d->c2_kh * d->c2_kw;
+      c.OH = s.oh2;
+      c.OW = s.ow2;
+      c.N = d->c2_out;
+      if (n > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
+      const unsigned grid = (unsigned)(n < cu_count() ? n : cu_count());
+      TimedLaunch tl(st, 2.0 * (double)n * s.oh2 * s.ow2 * d->c2_out * 64 * c.ntap);
+      hipLaunchKernelGGL((conv2x3_kernel<C2X3_MT>), dim3(grid), dim3(256), 0, st, c);
+      tl.done(st);
+      HONK_LAUNCH_CHECK("conv2x3_kernel");
+      cur = B;
+      other = A;
+    } else if (d->has_conv2) {  // model.py:190-193
       const bool fuse2 = d->p2_h == 2 && d->p2_w == 2;
       rc = conv(cur, t[2], t[3], other, n, d->c1_out, s.ph1, s.pw1, d->c2_out, d->c2_kh, d->c2_kw, d->c2_sh,
                 d->c2_sw, 1, st, fuse2, x3);

@@ -63,3 +63,20 @@ def test_cnn_x3_batch_invariance():
     m = module(cfg, params, "cnn-trad-pool2")
     full = run(m, x)
     assert np.array_equal(full, np.concatenate([run(m, x[:4]), run(m, x[4:])]))
+
+
+def test_cnn_x3_conv2_fast_path_multi_clip_per_block(monkeypatch):
+    # 300 clips > the 256-CU grid: conv2x3_kernel's persistent loop takes a second
+    # clip on some workgroups; the generic-GEMM conv2 (HONK_CNN_C2X3=0) agrees at the bar
+    name = "cnn-trad-pool2"
+    cfg = dict(ref_configs()[name], n_labels=12)
+    params = orc.make_params(cfg, 7)
+    x = np.random.Generator(np.random.PCG64(8)).standard_normal((300, 101, 40)).astype(np.float32)
+    m = module(cfg, params, name)
+    fast = run(m, x)
+    np.testing.assert_allclose(fast, orc.forward(params, cfg, x), atol=ATOL, rtol=0)
+    monkeypatch.setenv("HONK_CNN_C1X3", "0")  # generic-GEMM conv1 (NHWC epilogue) + conv2x3
+    np.testing.assert_allclose(run(m, x), fast, atol=ATOL, rtol=0)
+    monkeypatch.setenv("HONK_CNN_C2X3", "0")  # generic GEMMs for both convs
+    gen = run(m, x)
+    np.testing.assert_allclose(fast, gen, atol=ATOL, rtol=0)
