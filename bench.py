@@ -248,6 +248,62 @@ def measure_mode(prec, model, x, args, dev, barrier, hd, _native, orc, cfg, B, w
             "note": PREC_NOTES[prec]}
 
 
+def measure_c2(args, dev, barrier, hd, _native, orc, world, rank):
+    """Config C2 (BASELINE.json configs[1]): cnn-trad-pool2 eval forward, 65,536
+    clips per GPU, in bf16x3 (1e-4 parity) and fp32 MFMA, reported beside the res15
+    headline.  Roofline: algorithmic conv FLOP per launch over the conv kernels'
+    mean launch time (HIP events on the launch stream), vs bf16 peak / 3 (bf16x3)
+    or the fp32 MFMA peak."""
+    from honk_amd import model as hm
+    name = "cnn-trad-pool2"
+    cfg = dict(hm.find_config(name))
+    torch.manual_seed(0)
+    model = hm.find_model(name)(cfg).eval().to(dev)
+    B = 65536
+    g = torch.Generator(device=dev).manual_seed(4321 + rank)
+    x = torch.randn(B, 101, 40, device=dev, generator=g)
+    out = {"workload": "cnn-trad-pool2 eval forward (config C2), 65,536 clips per GPU", "per_gpu_batch": B}
+    for prec in ("bf16x3", "f32"):
+        model.honk_precision = prec
+        with torch.no_grad():
+            for _ in range(max(1, args.warmup)):
+                model(x)
+            torch.cuda.synchronize()
+            barrier()
+            _native.timing_enable(True)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                y = model(x)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            barrier()
+            kms, nl, kfl = _native.timing_read()
+            _native.timing_enable(False)
+        el = hd.max_over_ranks(t1 - t0, device=dev)
+        idx = list(range(0, B, B // 32))[:32]
+        ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}, cfg,
+                          x[idx].cpu().numpy())
+        got = y[idx].cpu().numpy()
+        peak = FP32_MFMA_PEAK_TFLOPS if prec == "f32" else BF16_MFMA_PEAK_TFLOPS / 3
+        ach = (kfl / max(nl, 1)) / (kms / max(nl, 1) * 1e-3) / 1e12 if nl else None
+        out[f"{prec}_mode"] = {
+            "value": round(world * B * args.steps / el, 1), "unit": "clips/s", "dtype": prec,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "roofline": {"bound": "mfma",
+                         "kernel": ("honk::cnn::conv1x3_kernel + conv2x3_kernel (bf16x3 convs, 3 bf16 MFMA "
+                                    "products per MAC; peak = bf16 peak / 3)" if prec == "bf16x3" else
+                                    "honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM convs, fp32 MFMA)"),
+                         "achieved": round(ach, 2) if ach else None, "peak": round(peak, 1), "unit": "TFLOP/s",
+                         "frac": round(ach / peak, 4) if ach else None, "launches": nl,
+                         "avg_launch_ms": round(kms / max(nl, 1), 4), "flop_per_launch": kfl / max(nl, 1)},
+            "parity": {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
+                       "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()),
+                       "sample_clips": len(idx)},
+            "note": PREC_NOTES.get(prec, "")}
+    del x
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -333,6 +389,10 @@ def main():
                 alts[f"{other}_mode"] = measure_mode(other, model, x, args, dev, barrier, hd, _native, orc, cfg,
                                                      B, world)
 
+    c2 = None
+    if is_res and not args.no_alt and not args.e2e:
+        c2 = measure_c2(args, dev, barrier, hd, _native, orc, world, rank)
+
     total = world * B * args.steps
     value = total / elapsed
     flop_clip = orc.flops_per_clip(cfg)
@@ -362,8 +422,9 @@ def main():
                          {"bound": "mfma",
                           "kernel": ("honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM conv/linear, fp32 MFMA)"
                                      if prec == "f32" else
-                                     "honk::cnn::conv_gemm_kernel<.., X3=true> (implicit-GEMM conv/linear, "
-                                     "3 bf16 MFMA products per MAC; peak = bf16 peak / 3)"),
+                                     "honk::cnn conv kernels in bf16x3 (conv1x3/conv2x3 for cnn-trad-pool2, "
+                                     "else conv_gemm_kernel<.., X3=true>; 3 bf16 MFMA products per MAC; "
+                                     "peak = bf16 peak / 3)"),
                           "achieved": round(achieved, 2) if achieved else None,
                           "peak": peak, "unit": "TFLOP/s",
                           "frac": round(achieved / peak, 4) if achieved else None,
@@ -374,6 +435,8 @@ def main():
                        "sample_clips": len(idx)},
         }
         res.update(alts)
+        if c2 is not None:
+            res["c2_cnn_trad_pool2"] = c2
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         print(json.dumps(res), flush=True)

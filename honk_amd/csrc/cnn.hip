@@ -325,6 +325,11 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ 
 // Epilogue: bias + ReLU, NCHW fp32 stores (flatten order of model.py:194).
 // ---------------------------------------------------------------------------- //
 constexpr int C2X3_IMG = 96 * 1024;  // LDS bytes of one half image (PH*PW*128 <= this)
+// HONK_C2_ABLATE (timing-only experiment builds, wrong results): bit 1 no image
+// DMA, 2 every k-step loads k-step 0's weights, 4 no A-fragment reads
+#ifndef HONK_C2_ABLATE
+#define HONK_C2_ABLATE 0
+#endif
 
 struct Conv2X3Args {
   const __bf16* in;    // [B][PH][PW][hi 64 | lo 64]
@@ -361,6 +366,7 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
   typedef uint4 AFr[MT][2];
   typedef uint4 WFr[2][2];
   auto loadA = [&](AFr& A, int delta) {
+    if constexpr (HONK_C2_ABLATE & 4) return;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int P = P0[m] + delta;
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int pt = 0; pt < 2; ++pt) Wr[j][pt] = wl[((s * 4 + j) * 2 + pt) * 64];
+      for (int pt = 0; pt < 2; ++pt) Wr[j][pt] = wl[(((HONK_C2_ABLATE & 2) ? 0 : s * 4 + j) * 2 + pt) * 64];
   };
   f32x4 acc[MT][2];
   auto mma = [&](const AFr& A, const WFr& Wr) {
@@ -401,7 +407,7 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
       for (int j = 0; j < 2; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int h = 0; h < 2; ++h) {
       __syncthreads();  // every wave is done reading the previous image
-      for (int pc = wave; pc < pieces; pc += 4) {
+      for (int pc = wave; pc < ((HONK_C2_ABLATE & 1) ? 0 : pieces); pc += 4) {
         const int st = __builtin_amdgcn_readfirstlane(min(pc * 64, chunks - 64));
         const int L = st + lane;
         const int P = L >> 3, c = (L & 7) ^ (P & 7);
@@ -414,6 +420,15 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
       const int s0 = h * a.ntap;
       AFr A0, A1;
       WFr W0, W1;
+      if constexpr (HONK_C2_ABLATE & 4) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) {
+            const unsigned v = 0x3f803f80u ^ (unsigned)(lane * 2654435761u + m * 40503u + pt);
+            A0[m][pt] = A1[m][pt] = uint4{v, v ^ 0x10001u, v ^ 0x20002u, v ^ 0x30003u};
+          }
+      }
       loadW(W0, s0);
       loadA(A0, 0);
       for (int t = 0; t < a.ntap; t += 2) {  // ntap even (host-checked)
