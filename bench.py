@@ -158,8 +158,10 @@ def train_bench(args, dev, rank, world, barrier):
                        "parallelism": f"dp{world}: one flat fp32 grad bucket all-reduce ({flat.numel} params)"},
             "final_loss": float(loss.item()),
             "roofline": None,
-            "note": "fwd/bwd compute runs on PyTorch autograd (MIOpen) on the device; native kernels: fused "
-                    "SGD + the all-reduce bucket. Native backward kernels are future work (DESIGN.md)."}),
+            "note": "native kernels: the block convs' forward / input grad / weight grad "
+                    "(honk_conv3x3_f32, honk_conv3x3_wgrad_f32), train-mode BatchNorm fwd/bwd "
+                    "(honk_bn_train_*), fused SGD over the flat all-reduced bucket; conv0, pooling, ReLU, "
+                    "residual, mean, Linear and the loss run on PyTorch autograd on the device"}),
               flush=True)
 
 

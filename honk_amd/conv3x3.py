@@ -1,0 +1,118 @@
+"""Training-mode res block convolutions on the gfx950 kernels (libhonk_hip.so).
+
+``conv3x3(x, w)`` is the ``nn.Conv2d(C, C, 3, padding=1, bias=False)`` of
+SpeechResModel's block stack (/root/reference/utils/model.py:94-98, use_dilation
+False: res8/res26 and -narrow) as an autograd function whose forward, input
+gradient and weight gradient are ``honk_conv3x3_f32`` / ``honk_conv3x3_wgrad_f32``;
+``batch_norm_train(x, bn)`` is the blocks' train-mode ``BatchNorm2d(affine=False)``
+(model.py:100, 117-118) on ``honk_bn_train_fwd/bwd_f32``.  The rest of the
+training graph (ReLU, residual, conv0, pooling, mean, Linear, loss) stays PyTorch
+autograd on the device, so ``utils/train.py``'s loop (train.py:131-134) runs
+unchanged.
+"""
+from __future__ import annotations
+
+import torch
+
+from honk_amd import _native
+
+CHANNELS = (19, 45)
+
+
+def supported(x, conv) -> bool:
+    """The native kernels cover dilation-1, padding-1, bias-free 3x3 convs with C in CHANNELS."""
+    return (x.is_cuda and x.dtype == torch.float32 and conv.weight.shape[0] in CHANNELS
+            and tuple(conv.dilation) == (1, 1) and tuple(conv.padding) == (1, 1) and conv.bias is None)
+
+
+def _conv(x, w, flip):
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    y = torch.empty_like(x)
+    _native.check(_native.load().honk_conv3x3_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W,
+                                                  1 if flip else 0, _native.stream_handle(x.device)),
+                  "honk_conv3x3_f32")
+    return y
+
+
+def _wgrad(x, dy):
+    x, dy = x.contiguous(), dy.contiguous()
+    B, C, H, W = x.shape
+    lib = _native.load()
+    dw = torch.empty(C, C, 3, 3, dtype=torch.float32, device=x.device)
+    nbytes = lib.honk_conv3x3_wgrad_workspace_bytes(B, C, H, W)
+    ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=x.device)
+    _native.check(lib.honk_conv3x3_wgrad_f32(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), B, C, H, W,
+                                             ws.data_ptr(), nbytes, _native.stream_handle(x.device)),
+                  "honk_conv3x3_wgrad_f32")
+    return dw
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        w = w.contiguous()
+        ctx.save_for_backward(x, w)
+        return _conv(x, w, flip=False)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = _conv(dy, w, flip=True) if ctx.needs_input_grad[0] else None
+        dw = _wgrad(x, dy) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+def conv3x3(x, w):
+    return _Conv3x3.apply(x, w)
+
+
+# -- train-mode BatchNorm2d(affine=False) (model.py:100, 117-118 in training) -------
+def _bn_ws(B, C, HW, device):
+    n = _native.load().honk_bn_train_workspace_bytes(B, C, HW)
+    return torch.empty(max(int(n), 1), dtype=torch.uint8, device=device), int(n)
+
+
+class _BatchNormTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, running_mean, running_var, momentum, eps):
+        x = x.contiguous()
+        B, C, H, W = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        ws, nb = _bn_ws(B, C, H * W, x.device)
+        rm = running_mean.data_ptr() if running_mean is not None else None
+        rv = running_var.data_ptr() if running_var is not None else None
+        _native.check(_native.load().honk_bn_train_fwd_f32(x.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                                                           invstd.data_ptr(), rm, rv, B, C, H * W, momentum, eps,
+                                                           ws.data_ptr(), nb, _native.stream_handle(x.device)),
+                      "honk_bn_train_fwd_f32")
+        ctx.save_for_backward(y, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, invstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        B, C, H, W = y.shape
+        dx = torch.empty_like(y)
+        ws, nb = _bn_ws(B, C, H * W, y.device)
+        _native.check(_native.load().honk_bn_train_bwd_f32(dy.data_ptr(), y.data_ptr(), invstd.data_ptr(),
+                                                           dx.data_ptr(), B, C, H * W, ws.data_ptr(), nb,
+                                                           _native.stream_handle(y.device)),
+                      "honk_bn_train_bwd_f32")
+        return dx, None, None, None, None
+
+
+def bn_supported(x, bn) -> bool:
+    return (x.is_cuda and x.dtype == torch.float32 and bn.training and not bn.affine
+            and bn.track_running_stats and bn.momentum is not None and x.shape[0] > 1)
+
+
+def batch_norm_train(x, bn):
+    """nn.BatchNorm2d.forward in training mode (affine=False, momentum set): the
+    module's num_batches_tracked bookkeeping, then the native normalisation."""
+    bn.num_batches_tracked.add_(1)
+    return _BatchNormTrain.apply(x, bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps))

@@ -51,6 +51,301 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
   }
 }
 
+// ---------------------------------------------------------------------------- //
+// Training-mode 3x3 convolutions of the res block stack (dilation 1, padding 1,
+// no bias; model.py:94-98 with use_dilation False), fp32 NCHW like the PyTorch
+// tensors around them (train-mode BatchNorm, ReLU, residual and the loss stay
+// PyTorch ops on the device):
+//   conv3x3_kernel<C,NP>: y = conv(x, w) (flip 0) or the input gradient
+//     dx = conv(dy, w'), w'[o][i][t] = w[i][o][8-t] (flip 1) -- the transform is
+//     applied while the weights are staged into LDS as [in][tap][out].
+//   wgrad3x3_kernel<C>: per-workgroup partial dW over its tiles; wsum_kernel adds
+//     the partials in a fixed order (deterministic, no atomics).
+// VALU direct convolution: 19 (45) channels are far from an MFMA tile (19 -> 32
+// is 2.8x the work), and gfx950's fp32 VALU FMA rate equals its fp32 MFMA rate.
+// A tile is a band of TH rows of one clip: its (TH+2) x (W+2) zero-padded input
+// rows of every channel are staged in LDS once; each thread owns NP output
+// pixels x all C outputs (weights read as LDS broadcasts, 4 per ds_read_b128).
+// ---------------------------------------------------------------------------- //
+constexpr int TC_XL = 64 * 1024;  // bytes of the staged input tile
+
+template <int C>
+struct TC {
+  static constexpr int CW = (C + 3) & ~3;  // output channels padded to a float4
+  static constexpr int WL = C * 9 * CW;    // floats of the staged weights
+};
+
+struct Conv3Args {
+  const float* x;  // [B][C][H][W]
+  const float* w;  // OIHW [C][C][3][3]
+  float* y;        // [B][C][H][W]
+  int B, H, W, TH, nband, flip;
+};
+
+template <int C, int NP>
+__global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
+  constexpr int CW = TC<C>::CW;
+  __shared__ __attribute__((aligned(16))) float wl[TC<C>::WL];
+  __shared__ __attribute__((aligned(16))) float xl[TC_XL / 4];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < TC<C>::WL; i += 256) {
+    const int o = i % CW, it = i / CW, in = it / 9, t = it - in * 9;
+    float v = 0.f;
+    if (o < C) v = a.flip ? a.w[(in * C + o) * 9 + 8 - t] : a.w[(o * C + in) * 9 + t];
+    wl[i] = v;
+  }
+  const int Wp = a.W + 2;
+  for (int tile = blockIdx.x; tile < a.B * a.nband; tile += gridDim.x) {
+    const int b = tile / a.nband, h0 = (tile - b * a.nband) * a.TH;
+    const int th = min(a.TH, a.H - h0), rows = th + 2, plane = rows * Wp;
+    __syncthreads();  // previous tile's readers done (and the weights staged)
+    const float* xb = a.x + (size_t)b * C * a.H * a.W;
+    for (int i = tid; i < C * plane; i += 256) {
+      const int c = i / plane, rc = i - c * plane, r = rc / Wp, col = rc - r * Wp;
+      const int h = h0 - 1 + r, w = col - 1;
+      xl[i] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
+    }
+    __syncthreads();
+    float acc[NP][CW];
+    int base[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int q = tid + k * 256;
+      const int r = q / a.W, col = q - r * a.W;
+      base[k] = q < th * a.W ? r * Wp + col : 0;
+#pragma unroll
+      for (int o = 0; o < CW; ++o) acc[k][o] = 0.f;
+    }
+    for (int ci = 0; ci < C; ++ci) {
+      const float* xc = xl + ci * plane;
+      const float4* wc = (const float4*)(wl + ci * 9 * CW);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = (t / 3) * Wp + (t % 3);
+        float xv[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) xv[k] = xc[base[k] + toff];
+#pragma unroll
+        for (int j = 0; j < CW / 4; ++j) {
+          const float4 w4 = wc[t * (CW / 4) + j];
+#pragma unroll
+          for (int k = 0; k < NP; ++k) {
+            acc[k][4 * j + 0] = fmaf(xv[k], w4.x, acc[k][4 * j + 0]);
+            acc[k][4 * j + 1] = fmaf(xv[k], w4.y, acc[k][4 * j + 1]);
+            acc[k][4 * j + 2] = fmaf(xv[k], w4.z, acc[k][4 * j + 2]);
+            acc[k][4 * j + 3] = fmaf(xv[k], w4.w, acc[k][4 * j + 3]);
+          }
+        }
+      }
+    }
+    float* yb = a.y + (size_t)b * C * a.H * a.W + (size_t)h0 * a.W;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int q = tid + k * 256;
+      if (q < th * a.W) {
+#pragma unroll
+        for (int o = 0; o < C; ++o) yb[(size_t)o * a.H * a.W + q] = acc[k][o];
+      }
+    }
+  }
+}
+
+struct WgradArgs {
+  const float* x;   // [B][C][H][W]
+  const float* dy;  // [B][C][H][W]
+  float* part;      // [gridDim.x][C][C][9] partial sums
+  int B, H, W, TH, nband;
+};
+
+// thread j < C*9 owns the weight column (in ci, tap t) for all C outputs:
+// per pixel one x read + CW/4 broadcast dy reads ([pixel][out] in LDS), CW FMAs
+template <int C>
+__global__ __launch_bounds__(256) void wgrad3x3_kernel(WgradArgs a) {
+  constexpr int CW = TC<C>::CW;
+  constexpr int NJ = (C * 9 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float xl[TC_XL / 4];
+  __shared__ __attribute__((aligned(16))) float dl[TC_XL / 4];
+  const int tid = threadIdx.x;
+  const int Wp = a.W + 2;
+  float acc[NJ][CW];
+#pragma unroll
+  for (int n = 0; n < NJ; ++n)
+#pragma unroll
+    for (int o = 0; o < CW; ++o) acc[n][o] = 0.f;
+  for (int tile = blockIdx.x; tile < a.B * a.nband; tile += gridDim.x) {
+    const int b = tile / a.nband, h0 = (tile - b * a.nband) * a.TH;
+    const int th = min(a.TH, a.H - h0), rows = th + 2, plane = rows * Wp, npx = th * a.W;
+    __syncthreads();
+    const float* xb = a.x + (size_t)b * C * a.H * a.W;
+    for (int i = tid; i < C * plane; i += 256) {
+      const int c = i / plane, rc = i - c * plane, r = rc / Wp, col = rc - r * Wp;
+      const int h = h0 - 1 + r, w = col - 1;
+      xl[i] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
+    }
+    const float* db = a.dy + (size_t)b * C * a.H * a.W + (size_t)h0 * a.W;
+    for (int i = tid; i < CW * npx; i += 256) {  // dy transposed to [pixel][out]
+      const int o = i / npx, p = i - o * npx;
+      dl[p * CW + o] = o < C ? db[(size_t)o * a.H * a.W + p] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < NJ; ++n) {
+      const int j = tid + n * 256;
+      if (j < C * 9) {
+        const int ci = j / 9, t = j - ci * 9;
+        const float* xc = xl + ci * plane + (t / 3) * Wp + (t % 3);
+        int p = 0;
+        for (int r = 0; r < th; ++r) {
+          for (int col = 0; col < a.W; ++col, ++p) {
+            const float xv = xc[r * Wp + col];
+            const float4* d4 = (const float4*)(dl + p * CW);
+#pragma unroll
+            for (int q = 0; q < CW / 4; ++q) {
+              const float4 d = d4[q];
+              acc[n][4 * q + 0] = fmaf(xv, d.x, acc[n][4 * q + 0]);
+              acc[n][4 * q + 1] = fmaf(xv, d.y, acc[n][4 * q + 1]);
+              acc[n][4 * q + 2] = fmaf(xv, d.z, acc[n][4 * q + 2]);
+              acc[n][4 * q + 3] = fmaf(xv, d.w, acc[n][4 * q + 3]);
+            }
+          }
+        }
+      }
+    }
+  }
+  float* pb = a.part + (size_t)blockIdx.x * C * C * 9;
+#pragma unroll
+  for (int n = 0; n < NJ; ++n) {
+    const int j = tid + n * 256;
+    if (j < C * 9) {
+#pragma unroll
+      for (int o = 0; o < C; ++o) pb[o * C * 9 + j] = acc[n][o];  // [o][ci][t]: j = ci*9 + t
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void wsum_kernel(const float* __restrict__ part, float* __restrict__ dw, int n,
+                                                   int nblk) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < nblk; ++k) s += part[(size_t)k * n + i];
+  dw[i] = s;
+}
+
+// ---------------------------------------------------------------------------- //
+// Train-mode BatchNorm2d(affine=False) of the res blocks (model.py:100,117-118 in
+// training): batch statistics over (B, H, W) per channel, running-stat update,
+// normalisation; backward dx = invstd (dy - mean(dy) - y mean(dy y)) with y = the
+// normalised output (affine=False: y IS x-hat).  PyTorch's NCHW kernels take one
+// workgroup row per channel (19 channels -> 9 ms per layer per 4096 clips);
+// here a channel's B planes are split over S workgroups, each reducing in fp64,
+// and a per-channel pass combines the S partials in a fixed order.
+// ---------------------------------------------------------------------------- //
+__device__ __forceinline__ double bn_block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+// part[c][s] = (sum a, sum a*b) over planes b of slice s of channel c, a = p[.], b = q[.]
+// (q == nullptr: b = a, i.e. the sum of squares)
+__global__ __launch_bounds__(256) void bn_partial_kernel(const float* __restrict__ p, const float* __restrict__ q,
+                                                         double* __restrict__ part, int B, int C, int HW, int S) {
+  __shared__ double red[4];
+  const int c = blockIdx.x, s = blockIdx.y;
+  const int b0 = (int)((int64_t)B * s / S), b1 = (int)((int64_t)B * (s + 1) / S);
+  double sa = 0.0, sab = 0.0;
+  for (int b = b0; b < b1; ++b) {
+    const size_t base = ((size_t)b * C + c) * HW;
+    for (int i = threadIdx.x; i < HW; i += 256) {
+      const float a = p[base + i];
+      const float bb = q ? q[base + i] : a;
+      sa += (double)a;
+      sab += (double)a * (double)bb;
+    }
+  }
+  sa = bn_block_sum(sa, red);
+  sab = bn_block_sum(sab, red);
+  if (threadIdx.x == 0) {
+    part[((size_t)c * S + s) * 2] = sa;
+    part[((size_t)c * S + s) * 2 + 1] = sab;
+  }
+}
+
+// forward: mean, invstd per channel; running stats (momentum, unbiased variance)
+__global__ void bn_stats_kernel(const double* __restrict__ part, float* __restrict__ mean, float* __restrict__ invstd,
+                                float* __restrict__ rmean, float* __restrict__ rvar, int C, int S, double n,
+                                float momentum, float eps) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < S; ++s) {
+    s1 += part[((size_t)c * S + s) * 2];
+    s2 += part[((size_t)c * S + s) * 2 + 1];
+  }
+  const double m = s1 / n;
+  double var = s2 / n - m * m;
+  if (var < 0.0) var = 0.0;
+  mean[c] = (float)m;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) {
+    rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * m);
+    rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * var * n / (n > 1.0 ? n - 1.0 : 1.0));
+  }
+}
+
+// backward: per-channel mean(dy), mean(dy*y)
+__global__ void bn_bstats_kernel(const double* __restrict__ part, float* __restrict__ mdy, float* __restrict__ mdyy,
+                                 int C, int S, double n) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < S; ++s) {
+    s1 += part[((size_t)c * S + s) * 2];
+    s2 += part[((size_t)c * S + s) * 2 + 1];
+  }
+  mdy[c] = (float)(s1 / n);
+  mdyy[c] = (float)(s2 / n);
+}
+
+// out = (a - u[c]) * v[c]                         (forward: y = (x - mean) invstd)
+// out = v[c] * (a - u[c] - b * w[c])              (backward: dx, a = dy, b = y)
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                       const float* __restrict__ u, const float* __restrict__ v,
+                                                       const float* __restrict__ w, float* __restrict__ out,
+                                                       int64_t total, int C, int HW) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)((i / HW) % C);
+  out[i] = b ? v[c] * (a[i] - u[c] - b[i] * w[c]) : (a[i] - u[c]) * v[c];
+}
+
+static int bn_slices(int B, int C) {
+  int S = (4 * 256 + C - 1) / C;  // ~4 workgroups per CU in total
+  if (S > B) S = B;
+  return S < 1 ? 1 : S;
+}
+
+// rows per tile: the staged input (C planes of (TH+2) x (W+2)) within TC_XL, the
+// tile's pixels within the NP pixels per thread, and (wgrad) its dy within TC_XL
+static int tc_rows(int C, int H, int W, int np) {
+  int th = TC_XL / 4 / (C * (W + 2)) - 2;
+  const int byp = (256 * np) / W;
+  if (th > byp) th = byp;
+  const int byd = TC_XL / 4 / (((C + 3) & ~3) * W);
+  if (th > byd) th = byd;
+  if (th > H) th = H;
+  return th;
+}
+static int tc_grid(int64_t tiles) {
+  const int64_t g = 2 * (int64_t)cu_count();
+  return (int)(tiles < g ? tiles : g);
+}
+
 }  // namespace train
 }  // namespace honk
 
@@ -66,5 +361,124 @@ extern "C" int honk_sgd_step_f32(float* params, const float* grads, float* momen
   hipLaunchKernelGGL(train::sgd_kernel, dim3((unsigned)cdiv(threads, 256)), dim3(256), 0, (hipStream_t)stream,
                      params, grads, momentum_buf, n, lr, momentum, weight_decay, grad_scale, nesterov);
   HONK_LAUNCH_CHECK("sgd_kernel");
+  return HONK_OK;
+}
+
+namespace {
+int tc_check(const void* a, const void* b, const void* c, int64_t batch, int32_t ch, int32_t h, int32_t w) {
+  if (!a || !b || !c) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 0 || h < 1 || w < 1) return fail(HONK_ERR_ARG, "bad conv3x3 shape (B=%lld H=%d W=%d)", (long long)batch, h, w);
+  if (ch != 19 && ch != 45) return fail(HONK_ERR_UNSUPPORTED, "conv3x3 training kernels: C=%d (19 or 45)", ch);
+  if (train::tc_rows(ch, h, w, ch == 19 ? 4 : 2) < 1) return fail(HONK_ERR_UNSUPPORTED, "conv3x3: width %d too large", w);
+  if (batch * (int64_t)h > 0x3fffffff) return fail(HONK_ERR_ARG, "conv3x3: batch too large");
+  return HONK_OK;
+}
+}  // namespace
+
+extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
+                                int32_t w_, int32_t flip, void* stream) {
+  int rc = tc_check(x, w, y, batch, c, h, w_);
+  if (rc) return rc;
+  if (batch == 0) return HONK_OK;
+  train::Conv3Args a;
+  a.x = x; a.w = w; a.y = y;
+  a.B = (int)batch; a.H = h; a.W = w_; a.flip = flip ? 1 : 0;
+  a.TH = train::tc_rows(c, h, w_, c == 19 ? 4 : 2);
+  a.nband = (h + a.TH - 1) / a.TH;
+  const int grid = train::tc_grid((int64_t)a.B * a.nband);
+  hipStream_t st = (hipStream_t)stream;
+  TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
+  if (c == 19) hipLaunchKernelGGL((train::conv3x3_kernel<19, 4>), dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((train::conv3x3_kernel<45, 2>), dim3(grid), dim3(256), 0, st, a);
+  tl.done(st);
+  HONK_LAUNCH_CHECK("conv3x3_kernel");
+  return HONK_OK;
+}
+
+extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_) {
+  if (batch < 1 || (c != 19 && c != 45) || h < 1 || w_ < 1) return 0;
+  const int th = train::tc_rows(c, h, w_, c == 19 ? 4 : 2);
+  if (th < 1) return 0;
+  const int64_t tiles = batch * ((h + th - 1) / th);
+  return (size_t)train::tc_grid(tiles) * c * c * 9 * sizeof(float);
+}
+
+extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
+                                      int32_t h, int32_t w_, void* workspace, size_t ws_bytes, void* stream) {
+  int rc = tc_check(x, dy, dw, batch, c, h, w_);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const int n = c * c * 9;
+  if (batch == 0) {
+    HONK_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)n * sizeof(float), st));
+    return HONK_OK;
+  }
+  const size_t need = honk_conv3x3_wgrad_workspace_bytes(batch, c, h, w_);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  train::WgradArgs a;
+  a.x = x; a.dy = dy; a.part = (float*)workspace;
+  a.B = (int)batch; a.H = h; a.W = w_;
+  a.TH = train::tc_rows(c, h, w_, c == 19 ? 4 : 2);
+  a.nband = (h + a.TH - 1) / a.TH;
+  const int grid = train::tc_grid((int64_t)a.B * a.nband);
+  TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
+  if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((train::wgrad3x3_kernel<45>), dim3(grid), dim3(256), 0, st, a);
+  tl.done(st);
+  HONK_LAUNCH_CHECK("wgrad3x3_kernel");
+  hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, (const float*)workspace, dw,
+                     n, grid);
+  HONK_LAUNCH_CHECK("wsum_kernel");
+  return HONK_OK;
+}
+
+extern "C" size_t honk_bn_train_workspace_bytes(int64_t batch, int32_t c, int64_t hw) {
+  if (batch < 1 || c < 1 || hw < 1) return 0;
+  return (size_t)c * train::bn_slices((int)batch, c) * 2 * sizeof(double) + (size_t)4 * c * sizeof(float);
+}
+
+extern "C" int honk_bn_train_fwd_f32(const float* x, float* y, float* mean, float* invstd, float* running_mean,
+                                     float* running_var, int64_t batch, int32_t c, int64_t hw, float momentum,
+                                     float eps, void* workspace, size_t ws_bytes, void* stream) {
+  if (!x || !y || !mean || !invstd || (!running_mean != !running_var)) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 1 || c < 1 || hw < 1 || hw > 0x7fffffff || batch > 0x7fffffff) return fail(HONK_ERR_ARG, "bad batchnorm shape");
+  const size_t need = honk_bn_train_workspace_bytes(batch, c, hw);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  const int S = train::bn_slices((int)batch, c);
+  double* part = (double*)workspace;
+  hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, x, (const float*)nullptr, part,
+                     (int)batch, c, (int)hw, S);
+  HONK_LAUNCH_CHECK("bn_partial_kernel");
+  hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)cdiv(c, 64)), dim3(64), 0, st, (const double*)part, mean,
+                     invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
+  HONK_LAUNCH_CHECK("bn_stats_kernel");
+  const int64_t total = batch * c * hw;
+  hipLaunchKernelGGL(train::bn_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, x,
+                     (const float*)nullptr, (const float*)mean, (const float*)invstd, (const float*)nullptr, y, total,
+                     c, (int)hw);
+  HONK_LAUNCH_CHECK("bn_apply_kernel");
+  return HONK_OK;
+}
+
+extern "C" int honk_bn_train_bwd_f32(const float* dy, const float* y, const float* invstd, float* dx, int64_t batch,
+                                     int32_t c, int64_t hw, void* workspace, size_t ws_bytes, void* stream) {
+  if (!dy || !y || !invstd || !dx) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 1 || c < 1 || hw < 1 || hw > 0x7fffffff || batch > 0x7fffffff) return fail(HONK_ERR_ARG, "bad batchnorm shape");
+  const size_t need = honk_bn_train_workspace_bytes(batch, c, hw);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  const int S = train::bn_slices((int)batch, c);
+  double* part = (double*)workspace;
+  float* m = (float*)(part + (size_t)c * S * 2);
+  hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, dy, y, part, (int)batch, c, (int)hw, S);
+  HONK_LAUNCH_CHECK("bn_partial_kernel");
+  hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)cdiv(c, 64)), dim3(64), 0, st, (const double*)part, m,
+                     m + c, c, S, (double)batch * (double)hw);
+  HONK_LAUNCH_CHECK("bn_bstats_kernel");
+  const int64_t total = batch * c * hw;
+  hipLaunchKernelGGL(train::bn_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, dy, y,
+                     (const float*)m, invstd, (const float*)(m + c), dx, total, c, (int)hw);
+  HONK_LAUNCH_CHECK("bn_apply_kernel");
   return HONK_OK;
 }

@@ -29,6 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import conv3x3 as _conv3x3
 
 
 class ConfigType(Enum):
@@ -147,12 +148,23 @@ class SpeechResModel(SerializableModule):
         # "f32": exact fp32 path (1e-4 logit parity); "bf16": bf16 activations/weights
         # with fp32 accumulation (configs C3/C4; parity = top-1 agreement)
         self.honk_precision = "f32"
+        # training on ROCm tensors: block convs on the gfx950 kernels (False: MIOpen)
+        self.honk_native_train = True
 
     # -- reference forward (CPU tensors / training mode): model.py:104-121 --
-    def _torch_forward(self, x):
+    # native_convs: training on a ROCm tensor runs the block convs (conv1..convN)
+    # on honk_conv3x3_f32 / honk_conv3x3_wgrad_f32 where they cover the shape
+    # (dilation 1, 19 or 45 maps) and the train-mode BatchNorms on honk_bn_train_*
+    # (honk_amd/conv3x3.py); ReLU, residual, conv0, pool, mean, Linear and the loss
+    # stay PyTorch autograd
+    def _torch_forward(self, x, native_convs=False):
         x = x.unsqueeze(1)
         for i in range(self.n_layers + 1):
-            y = F.relu(getattr(self, "conv{}".format(i))(x))
+            conv = getattr(self, "conv{}".format(i))
+            if native_convs and i > 0 and _conv3x3.supported(x, conv):
+                y = F.relu(_conv3x3.conv3x3(x, conv.weight))
+            else:
+                y = F.relu(conv(x))
             if i == 0:
                 if hasattr(self, "pool"):
                     y = self.pool(y)
@@ -163,7 +175,11 @@ class SpeechResModel(SerializableModule):
             else:
                 x = y
             if i > 0:
-                x = getattr(self, "bn{}".format(i))(x)
+                bn = getattr(self, "bn{}".format(i))
+                if native_convs and _conv3x3.bn_supported(x, bn):
+                    x = _conv3x3.batch_norm_train(x, bn)
+                else:
+                    x = bn(x)
         x = x.view(x.size(0), x.size(1), -1)  # shape: (batch, feats, o3)
         x = torch.mean(x, 2)
         return self.output(x)
@@ -233,7 +249,7 @@ class SpeechResModel(SerializableModule):
     def forward(self, x):
         if _native_ready(x, self):
             return self._native_forward(x)
-        return self._torch_forward(x)
+        return self._torch_forward(x, native_convs=x.is_cuda and self.honk_native_train)
 
 
 class SpeechModel(SerializableModule):

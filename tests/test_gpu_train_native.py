@@ -1,0 +1,110 @@
+"""GPU: the training-mode res block convolutions on honk_conv3x3_f32 /
+honk_conv3x3_wgrad_f32 (honk_amd/conv3x3.py) against PyTorch's own conv
+forward / input gradient / weight gradient, and one full training step of the
+models whose block convs they replace (res8, res26-narrow: loss and every
+parameter gradient vs the all-PyTorch step, utils/train.py:131-134)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from honk_amd import _native
+from honk_amd import conv3x3 as hc
+from honk_amd import model as hm
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _native.load()
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("C,B,H,W", [(19, 3, 50, 20), (45, 2, 25, 13), (19, 1, 7, 5), (45, 3, 50, 20), (19, 5, 101, 40)])
+def test_conv3x3_kernels_match_torch(C, B, H, W):
+    g = torch.Generator(device=DEV).manual_seed(C * 100 + H)
+    x = torch.randn(B, C, H, W, device=DEV, generator=g)
+    w = torch.randn(C, C, 3, 3, device=DEV, generator=g) * 0.1
+    dy = torch.randn(B, C, H, W, device=DEV, generator=g)
+    y = hc._conv(x, w, flip=False)
+    torch.testing.assert_close(y, F.conv2d(x, w, padding=1), rtol=1e-5, atol=1e-5)
+    dx = hc._conv(dy, w, flip=True)
+    ref_dx = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=1)
+    torch.testing.assert_close(dx, ref_dx, rtol=1e-5, atol=1e-5)
+    dw = hc._wgrad(x, dy)
+    ref_dw = torch.nn.grad.conv2d_weight(x, w.shape, dy, padding=1)
+    assert _rel(dw, ref_dw) < 1e-5, _rel(dw, ref_dw)
+
+
+@pytest.mark.parametrize("B,C,H,W", [(4096 // 64, 19, 50, 20), (3, 45, 25, 13), (2, 19, 7, 5)])
+def test_batchnorm_train_matches_torch(B, C, H, W):
+    g = torch.Generator(device=DEV).manual_seed(B + C)
+    x = (torch.randn(B, C, H, W, device=DEV, generator=g) * 3 + 1.5).requires_grad_(True)
+    dy = torch.randn(B, C, H, W, device=DEV, generator=g)
+    bn_n, bn_t = torch.nn.BatchNorm2d(C, affine=False).to(DEV), torch.nn.BatchNorm2d(C, affine=False).to(DEV)
+    y = hc.batch_norm_train(x, bn_n)
+    (dxn,) = torch.autograd.grad(y, x, dy)
+    x64 = x.detach().double().cpu().requires_grad_(True)
+    bn64 = torch.nn.BatchNorm2d(C, affine=False).double()
+    y64 = bn64(x64)
+    (dx64,) = torch.autograd.grad(y64, x64, dy.double().cpu())
+    yt = bn_t(x)
+    (dxt,) = torch.autograd.grad(yt, x, dy)
+    assert _rel(y, y64) < 1e-6 and _rel(dxn, dx64) <= max(_rel(dxt, dx64), 1e-5)
+    torch.testing.assert_close(bn_n.running_mean, bn_t.running_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(bn_n.running_var, bn_t.running_var, rtol=1e-5, atol=1e-6)
+    assert int(bn_n.num_batches_tracked) == int(bn_t.num_batches_tracked) == 1
+
+
+def test_wgrad_deterministic():
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(64, 19, 50, 20, device=DEV, generator=g)
+    dy = torch.randn(64, 19, 50, 20, device=DEV, generator=g)
+    assert torch.equal(hc._wgrad(x, dy), hc._wgrad(x, dy))
+
+
+# bar: relative to the float64 step.  res8 at this seed has a channel that is dead
+# (all <= 0 before ReLU) after conv1 in float64; fp32 rounding differences of
+# ~1e-6 at its exact zeros flip ReLU masks, and train-mode BatchNorm (variance
+# ~0, sigma = sqrt(eps)) amplifies them ~300x per layer in the backward pass
+# (exp/diag_train2.py / diag_train3.py: the native forward is within 1e-6 of
+# float64 at every layer; dgrad and wgrad alone leave every gradient at 1e-6)
+@pytest.mark.parametrize("name,B,bar", [("res26-narrow", 8, 1e-3), ("res8-narrow", 4, 1e-3), ("res8", 6, 1e-2)])
+def test_train_step_grads_match_pytorch(name, B, bar):
+    # float64 CPU step = the reference; every gradient of the native-conv step must
+    # be within 1e-3 relative of it or no farther than the all-PyTorch (MIOpen) fp32
+    # step's (train-mode BatchNorm backward through 24 layers amplifies fp32
+    # rounding: measured native 1-3e-4, MIOpen 1e-3 .. 2e-2 on res26-narrow)
+    torch.manual_seed(0)
+    cfg = dict(hm.find_config(name))
+    m = hm.find_model(name)(cfg).to(DEV).train()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(B, 101, 40, device=DEV, generator=g)
+    y = torch.randint(0, cfg["n_labels"], (B,), device=DEV, generator=g)
+
+    def step(mod, xx, yy):
+        mod.zero_grad()
+        loss = F.cross_entropy(mod(xx), yy)
+        loss.backward()
+        return loss.detach().double().cpu(), {k: p.grad.detach().double().cpu() for k, p in mod.named_parameters()}
+
+    res = {}
+    for native in (True, False):
+        m.honk_native_train = native
+        res[native] = step(m, x, y)
+    m64 = hm.find_model(name)(cfg).double().train()
+    m64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in m.state_dict().items()})
+    l64, g64 = step(m64, x.double().cpu(), y.cpu())
+    (ln, gn), (lt, gt) = res[True], res[False]
+    assert abs(float(ln - l64)) <= max(3 * abs(float(lt - l64)), 1e-5)
+    for k in g64:
+        en, et = _rel(gn[k], g64[k]), _rel(gt[k], g64[k])
+        print(f"{name} {k}: native {en:.2e}  pytorch-fp32 {et:.2e}")
+        assert en <= max(et, bar), (k, en, et)
