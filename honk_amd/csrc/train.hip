@@ -82,6 +82,8 @@ struct Conv3Args {
   int B, H, W, TH, nband, flip;
 };
 
+typedef float tf2 __attribute__((ext_vector_type(2)));
+
 template <int C, int NP>
 __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
   constexpr int CW = TC<C>::CW;
@@ -106,7 +108,8 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
       xl[i] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
     }
     __syncthreads();
-    float acc[NP][CW];
+    // packed fp32 FMA (v_pk_fma_f32): output channel pairs share the pixel's input
+    tf2 acc[NP][CW / 2];
     int base[NP];
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
       const int r = q / a.W, col = q - r * a.W;
       base[k] = q < th * a.W ? r * Wp + col : 0;
 #pragma unroll
-      for (int o = 0; o < CW; ++o) acc[k][o] = 0.f;
+      for (int o = 0; o < CW / 2; ++o) acc[k][o] = tf2{0.f, 0.f};
     }
     for (int ci = 0; ci < C; ++ci) {
       const float* xc = xl + ci * plane;
@@ -122,18 +125,20 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int toff = (t / 3) * Wp + (t % 3);
-        float xv[NP];
+        tf2 xv[NP];
 #pragma unroll
-        for (int k = 0; k < NP; ++k) xv[k] = xc[base[k] + toff];
+        for (int k = 0; k < NP; ++k) {
+          const float v = xc[base[k] + toff];
+          xv[k] = tf2{v, v};
+        }
 #pragma unroll
         for (int j = 0; j < CW / 4; ++j) {
           const float4 w4 = wc[t * (CW / 4) + j];
+          const tf2 wa = tf2{w4.x, w4.y}, wb = tf2{w4.z, w4.w};
 #pragma unroll
           for (int k = 0; k < NP; ++k) {
-            acc[k][4 * j + 0] = fmaf(xv[k], w4.x, acc[k][4 * j + 0]);
-            acc[k][4 * j + 1] = fmaf(xv[k], w4.y, acc[k][4 * j + 1]);
-            acc[k][4 * j + 2] = fmaf(xv[k], w4.z, acc[k][4 * j + 2]);
-            acc[k][4 * j + 3] = fmaf(xv[k], w4.w, acc[k][4 * j + 3]);
+            acc[k][2 * j] = __builtin_elementwise_fma(xv[k], wa, acc[k][2 * j]);
+            acc[k][2 * j + 1] = __builtin_elementwise_fma(xv[k], wb, acc[k][2 * j + 1]);
           }
         }
       }
@@ -144,7 +149,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
       const int q = tid + k * 256;
       if (q < th * a.W) {
 #pragma unroll
-        for (int o = 0; o < C; ++o) yb[(size_t)o * a.H * a.W + q] = acc[k][o];
+        for (int o = 0; o < C; ++o) yb[(size_t)o * a.H * a.W + q] = acc[k][o >> 1][o & 1];
       }
     }
   }
@@ -153,72 +158,92 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
 struct WgradArgs {
   const float* x;   // [B][C][H][W]
   const float* dy;  // [B][C][H][W]
-  float* part;      // [gridDim.x][C][C][9] partial sums
+  float* part;      // [gridDim.x][NG][C][C][9] partial sums
   int B, H, W, TH, nband;
 };
 
-// thread j < C*9 owns the weight column (in ci, tap t) for all C outputs:
-// per pixel one x read + CW/4 broadcast dy reads ([pixel][out] in LDS), CW FMAs
+// wgrad: 512 threads = NG groups of TG threads (+ idle); group g takes the tile's
+// pixels p = g, g + NG, ..; thread (g, u) owns PJ consecutive weight columns
+// j = (in ci, tap t) = PJ u .. PJ u + PJ-1 for all C outputs.  Per pixel: PJ x
+// reads + CW/4 dy reads ([pixel][out] in LDS) for PJ*CW FMAs (packed).
+constexpr int WG_PJ = 4;
 template <int C>
-__global__ __launch_bounds__(256) void wgrad3x3_kernel(WgradArgs a) {
-  constexpr int CW = TC<C>::CW;
-  constexpr int NJ = (C * 9 + 255) / 256;
+struct WG {
+  static constexpr int TG = (C * 9 + WG_PJ - 1) / WG_PJ;  // threads per group
+  static constexpr int NG = 512 / TG;                     // pixel groups
+};
+
+template <int C>
+__global__ __launch_bounds__(512) void wgrad3x3_kernel(WgradArgs a) {
+  constexpr int CW = TC<C>::CW, TG = WG<C>::TG, NG = WG<C>::NG, PJ = WG_PJ;
   __shared__ __attribute__((aligned(16))) float xl[TC_XL / 4];
   __shared__ __attribute__((aligned(16))) float dl[TC_XL / 4];
   const int tid = threadIdx.x;
+  const int grp = tid / TG, u = tid - grp * TG;
+  const bool active = grp < NG;
   const int Wp = a.W + 2;
-  float acc[NJ][CW];
+  tf2 acc[PJ][CW / 2];
+  int jo[PJ];  // per owned column: LDS offset of (ci, tap) in the tile (row 0, col 0), -1 if none
 #pragma unroll
-  for (int n = 0; n < NJ; ++n)
+  for (int n = 0; n < PJ; ++n) {
 #pragma unroll
-    for (int o = 0; o < CW; ++o) acc[n][o] = 0.f;
+    for (int o = 0; o < CW / 2; ++o) acc[n][o] = tf2{0.f, 0.f};
+  }
   for (int tile = blockIdx.x; tile < a.B * a.nband; tile += gridDim.x) {
     const int b = tile / a.nband, h0 = (tile - b * a.nband) * a.TH;
     const int th = min(a.TH, a.H - h0), rows = th + 2, plane = rows * Wp, npx = th * a.W;
     __syncthreads();
     const float* xb = a.x + (size_t)b * C * a.H * a.W;
-    for (int i = tid; i < C * plane; i += 256) {
+    for (int i = tid; i < C * plane; i += 512) {
       const int c = i / plane, rc = i - c * plane, r = rc / Wp, col = rc - r * Wp;
       const int h = h0 - 1 + r, w = col - 1;
       xl[i] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
     }
     const float* db = a.dy + (size_t)b * C * a.H * a.W + (size_t)h0 * a.W;
-    for (int i = tid; i < CW * npx; i += 256) {  // dy transposed to [pixel][out]
+    for (int i = tid; i < CW * npx; i += 512) {  // dy transposed to [pixel][out]
       const int o = i / npx, p = i - o * npx;
       dl[p * CW + o] = o < C ? db[(size_t)o * a.H * a.W + p] : 0.f;
     }
     __syncthreads();
+    if (active) {
 #pragma unroll
-    for (int n = 0; n < NJ; ++n) {
-      const int j = tid + n * 256;
-      if (j < C * 9) {
+      for (int n = 0; n < PJ; ++n) {
+        const int j = PJ * u + n;
         const int ci = j / 9, t = j - ci * 9;
-        const float* xc = xl + ci * plane + (t / 3) * Wp + (t % 3);
-        int p = 0;
-        for (int r = 0; r < th; ++r) {
-          for (int col = 0; col < a.W; ++col, ++p) {
-            const float xv = xc[r * Wp + col];
-            const float4* d4 = (const float4*)(dl + p * CW);
+        jo[n] = j < C * 9 ? ci * plane + (t / 3) * Wp + (t % 3) : 0;
+      }
+      for (int p = grp; p < npx; p += NG) {
+        const int r = p / a.W, col = p - r * a.W;
+        const int po = r * Wp + col;
+        tf2 xv[PJ];
 #pragma unroll
-            for (int q = 0; q < CW / 4; ++q) {
-              const float4 d = d4[q];
-              acc[n][4 * q + 0] = fmaf(xv, d.x, acc[n][4 * q + 0]);
-              acc[n][4 * q + 1] = fmaf(xv, d.y, acc[n][4 * q + 1]);
-              acc[n][4 * q + 2] = fmaf(xv, d.z, acc[n][4 * q + 2]);
-              acc[n][4 * q + 3] = fmaf(xv, d.w, acc[n][4 * q + 3]);
-            }
+        for (int n = 0; n < PJ; ++n) {
+          const float v = xl[jo[n] + po];
+          xv[n] = tf2{v, v};
+        }
+        const float4* d4 = (const float4*)(dl + p * CW);
+#pragma unroll
+        for (int q = 0; q < CW / 4; ++q) {
+          const float4 d = d4[q];
+          const tf2 da = tf2{d.x, d.y}, dbv = tf2{d.z, d.w};
+#pragma unroll
+          for (int n = 0; n < PJ; ++n) {
+            acc[n][2 * q] = __builtin_elementwise_fma(xv[n], da, acc[n][2 * q]);
+            acc[n][2 * q + 1] = __builtin_elementwise_fma(xv[n], dbv, acc[n][2 * q + 1]);
           }
         }
       }
     }
   }
-  float* pb = a.part + (size_t)blockIdx.x * C * C * 9;
+  if (active) {
+    float* pb = a.part + ((size_t)blockIdx.x * NG + grp) * C * C * 9;
 #pragma unroll
-  for (int n = 0; n < NJ; ++n) {
-    const int j = tid + n * 256;
-    if (j < C * 9) {
+    for (int n = 0; n < PJ; ++n) {
+      const int j = PJ * u + n;
+      if (j < C * 9) {
 #pragma unroll
-      for (int o = 0; o < C; ++o) pb[o * C * 9 + j] = acc[n][o];  // [o][ci][t]: j = ci*9 + t
+        for (int o = 0; o < C; ++o) pb[o * C * 9 + j] = acc[n][o >> 1][o & 1];  // [o][ci][t]: j = ci*9 + t
+      }
     }
   }
 }
@@ -330,16 +355,18 @@ static int bn_slices(int B, int C) {
   return S < 1 ? 1 : S;
 }
 
-// rows per tile: the staged input (C planes of (TH+2) x (W+2)) within TC_XL, the
-// tile's pixels within the NP pixels per thread, and (wgrad) its dy within TC_XL
-static int tc_rows(int C, int H, int W, int np) {
+// rows per tile: the staged input (C planes of (TH+2) x (W+2)) and (wgrad) its dy
+// within TC_XL, at most 1024 pixels (4 per thread); bands balanced over the clip
+static int tc_rows(int C, int H, int W) {
   int th = TC_XL / 4 / (C * (W + 2)) - 2;
-  const int byp = (256 * np) / W;
+  const int byp = (C <= 20 ? 1024 : 512) / W;  // conv3x3_kernel: NP <= 4 (19 maps) / 2 (45 maps)
   if (th > byp) th = byp;
   const int byd = TC_XL / 4 / (((C + 3) & ~3) * W);
   if (th > byd) th = byd;
   if (th > H) th = H;
-  return th;
+  if (th < 1) return 0;
+  const int nb = (H + th - 1) / th;
+  return (H + nb - 1) / nb;
 }
 static int tc_grid(int64_t tiles) {
   const int64_t g = 2 * (int64_t)cu_count();
@@ -369,7 +396,7 @@ int tc_check(const void* a, const void* b, const void* c, int64_t batch, int32_t
   if (!a || !b || !c) return fail(HONK_ERR_ARG, "null pointer argument");
   if (batch < 0 || h < 1 || w < 1) return fail(HONK_ERR_ARG, "bad conv3x3 shape (B=%lld H=%d W=%d)", (long long)batch, h, w);
   if (ch != 19 && ch != 45) return fail(HONK_ERR_UNSUPPORTED, "conv3x3 training kernels: C=%d (19 or 45)", ch);
-  if (train::tc_rows(ch, h, w, ch == 19 ? 4 : 2) < 1) return fail(HONK_ERR_UNSUPPORTED, "conv3x3: width %d too large", w);
+  if (train::tc_rows(ch, h, w) < 1) return fail(HONK_ERR_UNSUPPORTED, "conv3x3: width %d too large", w);
   if (batch * (int64_t)h > 0x3fffffff) return fail(HONK_ERR_ARG, "conv3x3: batch too large");
   return HONK_OK;
 }
@@ -383,13 +410,21 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   train::Conv3Args a;
   a.x = x; a.w = w; a.y = y;
   a.B = (int)batch; a.H = h; a.W = w_; a.flip = flip ? 1 : 0;
-  a.TH = train::tc_rows(c, h, w_, c == 19 ? 4 : 2);
+  a.TH = train::tc_rows(c, h, w_);
   a.nband = (h + a.TH - 1) / a.TH;
   const int grid = train::tc_grid((int64_t)a.B * a.nband);
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (c == 19) hipLaunchKernelGGL((train::conv3x3_kernel<19, 4>), dim3(grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((train::conv3x3_kernel<45, 2>), dim3(grid), dim3(256), 0, st, a);
+  const int np = (int)cdiv((int64_t)a.TH * w_, 256);  // output pixels per thread
+  if (c == 19) {
+    if (np <= 1) hipLaunchKernelGGL((train::conv3x3_kernel<19, 1>), dim3(grid), dim3(256), 0, st, a);
+    else if (np == 2) hipLaunchKernelGGL((train::conv3x3_kernel<19, 2>), dim3(grid), dim3(256), 0, st, a);
+    else if (np == 3) hipLaunchKernelGGL((train::conv3x3_kernel<19, 3>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((train::conv3x3_kernel<19, 4>), dim3(grid), dim3(256), 0, st, a);
+  } else {
+    if (np <= 1) hipLaunchKernelGGL((train::conv3x3_kernel<45, 1>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((train::conv3x3_kernel<45, 2>), dim3(grid), dim3(256), 0, st, a);
+  }
   tl.done(st);
   HONK_LAUNCH_CHECK("conv3x3_kernel");
   return HONK_OK;
@@ -397,10 +432,11 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
 
 extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_) {
   if (batch < 1 || (c != 19 && c != 45) || h < 1 || w_ < 1) return 0;
-  const int th = train::tc_rows(c, h, w_, c == 19 ? 4 : 2);
+  const int th = train::tc_rows(c, h, w_);
   if (th < 1) return 0;
   const int64_t tiles = batch * ((h + th - 1) / th);
-  return (size_t)train::tc_grid(tiles) * c * c * 9 * sizeof(float);
+  const int ng = c == 19 ? train::WG<19>::NG : train::WG<45>::NG;
+  return (size_t)train::tc_grid(tiles) * ng * c * c * 9 * sizeof(float);
 }
 
 extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
@@ -418,16 +454,17 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
   train::WgradArgs a;
   a.x = x; a.dy = dy; a.part = (float*)workspace;
   a.B = (int)batch; a.H = h; a.W = w_;
-  a.TH = train::tc_rows(c, h, w_, c == 19 ? 4 : 2);
+  a.TH = train::tc_rows(c, h, w_);
   a.nband = (h + a.TH - 1) / a.TH;
   const int grid = train::tc_grid((int64_t)a.B * a.nband);
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((train::wgrad3x3_kernel<45>), dim3(grid), dim3(256), 0, st, a);
+  if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((train::wgrad3x3_kernel<45>), dim3(grid), dim3(512), 0, st, a);
   tl.done(st);
   HONK_LAUNCH_CHECK("wgrad3x3_kernel");
+  const int ng = c == 19 ? train::WG<19>::NG : train::WG<45>::NG;
   hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, (const float*)workspace, dw,
-                     n, grid);
+                     n, grid * ng);
   HONK_LAUNCH_CHECK("wsum_kernel");
   return HONK_OK;
 }
