@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
 struct WgradArgs {
   const float* x;   // [B][C][H][W]
   const float* dy;  // [B][C][H][W]
-  float* part;      // [gridDim.x][NG][C][C][9] partial sums
+  float* part;      // [gridDim.x][C][C][9] partial sums
   int B, H, W, TH, nband;
 };
 
@@ -235,26 +235,45 @@ __global__ __launch_bounds__(512) void wgrad3x3_kernel(WgradArgs a) {
       }
     }
   }
-  if (active) {
-    float* pb = a.part + ((size_t)blockIdx.x * NG + grp) * C * C * 9;
+  // the NG groups' columns summed in LDS (fixed order), 4 output channels at a time
+  __syncthreads();  // every group is done with the tile images
+  float* red = xl;  // NG x (C*9) x 4 floats
+  float* pb = a.part + (size_t)blockIdx.x * C * C * 9;
 #pragma unroll
-    for (int n = 0; n < PJ; ++n) {
-      const int j = PJ * u + n;
-      if (j < C * 9) {
+  for (int q = 0; q < CW / 4; ++q) {
+    if (active) {
 #pragma unroll
-        for (int o = 0; o < C; ++o) pb[o * C * 9 + j] = acc[n][o >> 1][o & 1];  // [o][ci][t]: j = ci*9 + t
+      for (int n = 0; n < PJ; ++n) {
+        const int j = PJ * u + n;
+        if (j < C * 9)
+          *(float4*)(red + ((size_t)grp * C * 9 + j) * 4) =
+              float4{acc[n][2 * q].x, acc[n][2 * q].y, acc[n][2 * q + 1].x, acc[n][2 * q + 1].y};
       }
     }
+    __syncthreads();
+    for (int idx = tid; idx < C * 9 * 4; idx += 512) {
+      float v = 0.f;
+      for (int g = 0; g < NG; ++g) v += red[(size_t)g * C * 9 * 4 + idx];
+      const int o = 4 * q + (idx & 3), j = idx >> 2;
+      if (o < C) pb[o * C * 9 + j] = v;  // [o][ci][t]: j = ci*9 + t
+    }
+    __syncthreads();
   }
 }
 
+// dw[i] = sum over the nblk per-workgroup partials, fixed order: 64 outputs per
+// workgroup, 4 strands over k (k = strand mod 4) combined in LDS
 __global__ __launch_bounds__(256) void wsum_kernel(const float* __restrict__ part, float* __restrict__ dw, int n,
                                                    int nblk) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  __shared__ float red[4][64];
+  const int il = threadIdx.x & 63, strand = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + il;
   float s = 0.f;
-  for (int k = 0; k < nblk; ++k) s += part[(size_t)k * n + i];
-  dw[i] = s;
+  if (i < n)
+    for (int k = strand; k < nblk; k += 4) s += part[(size_t)k * n + i];
+  red[strand][il] = s;
+  __syncthreads();
+  if (strand == 0 && i < n) dw[i] = (red[0][il] + red[1][il]) + (red[2][il] + red[3][il]);
 }
 
 // ---------------------------------------------------------------------------- //
@@ -435,8 +454,7 @@ extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, i
   const int th = train::tc_rows(c, h, w_);
   if (th < 1) return 0;
   const int64_t tiles = batch * ((h + th - 1) / th);
-  const int ng = c == 19 ? train::WG<19>::NG : train::WG<45>::NG;
-  return (size_t)train::tc_grid(tiles) * ng * c * c * 9 * sizeof(float);
+  return (size_t)train::tc_grid(tiles) * c * c * 9 * sizeof(float);
 }
 
 extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
@@ -462,9 +480,8 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
   else hipLaunchKernelGGL((train::wgrad3x3_kernel<45>), dim3(grid), dim3(512), 0, st, a);
   tl.done(st);
   HONK_LAUNCH_CHECK("wgrad3x3_kernel");
-  const int ng = c == 19 ? train::WG<19>::NG : train::WG<45>::NG;
-  hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, (const float*)workspace, dw,
-                     n, grid * ng);
+  hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, 64)), dim3(256), 0, st, (const float*)workspace, dw,
+                     n, grid);
   HONK_LAUNCH_CHECK("wsum_kernel");
   return HONK_OK;
 }
