@@ -89,7 +89,9 @@ size_t honk_cnn_workspace_bytes(const honk_cnn_desc* d, int64_t batch);
  * tensors[] (device fp32, contiguous; NULL for absent layers), fixed order of 12:
  *   conv1.weight, conv1.bias, conv2.weight, conv2.bias, lin.weight, lin.bias,
  *   dnn1.weight, dnn1.bias, dnn2.weight, dnn2.bias, output.weight, output.bias
- * No packing: OIHW weights are already the [N][K] operand of the implicit GEMM.
+ * No separate pack call: OIHW weights are the [N][K] operand of the generic implicit GEMM; the
+ * bf16x3 cnn-trad-pool2 path splits conv2's weights into hi/lo fragments inside the workspace
+ * on every call (one small launch) and conv1's while staging them into registers.
  */
 int honk_cnn_forward(const honk_cnn_desc* d, const float* const* tensors, const float* x,
                      float* logits, int64_t batch, void* workspace, size_t workspace_bytes,
