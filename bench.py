@@ -205,8 +205,8 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model):
     per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1)) / L
     bw = per_clip * clips / avg_s / 1e9 if nl else None
     mf = (kfl * (3 if sp == 2 else 1) / max(nl, 1)) / avg_s / 1e12 if nl else None
-    # 45-map bf16 runs the per-dy-stage kernel; bf16x3 and narrow maps the row-band kernel
-    fam = "block16_kernel" if (sp == 1 and CP == 48) else "block16r_kernel"
+    # every res config runs the row-band kernel (HONK_RES_ROWBAND=0: the per-dy-stage one)
+    fam = "block16_kernel" if os.environ.get("HONK_RES_ROWBAND") == "0" else "block16r_kernel"
     return {"bound": "hbm", "kernel": f"honk::res::{fam}<..., SP={sp}> (dilated 3x3 conv, bf16 MFMA)",
             "achieved": round(bw, 1) if bw else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(bw / HBM_PEAK_GBS, 4) if bw else None,

@@ -741,6 +741,8 @@ static int dispatch_block16(const Plan& p, int SP, const Block16Args& a, hipStre
 // Row-band kernel plan (res_bf16r.inc): same (NT, MT) as plan_block16; TH rows of
 // one dilation class per tile, limited by the tile's pixels and by the staging
 // image (TH + 2 rows); th = 0: not applicable (fall back to block16_kernel).
+// (3,3,1) (45-map bf16): 0.97 -> 0.89 ms per 4096-clip res15 launch vs the
+// per-dy-stage kernel (exp/ab_rowband.py); its LAST+RES variant spills 14 VGPRs.
 // HONK_RES_ROWBAND=0 selects the per-dy-stage kernel for A/B runs.
 struct PlanR {
   int NT, MT, TH;
@@ -750,7 +752,6 @@ static PlanR plan_block16r(const Layout& L, int SP) {
   PlanR r{p.NT, p.MT, 0};
   if (const char* e = getenv("HONK_RES_ROWBAND"))
     if (atoi(e) == 0) return r;
-  if (SP == 1 && p.NT == 3) return r;  // (3,3,1): 3 x aoff spills at 2 waves/SIMD -> per-dy-stage kernel
   const int MP = 16 * g16_nw(SP) * p.MT;
   const int rpx = g16r_rpx(L.NT, MP / 128, SP);
   int th = MP / L.W;
@@ -790,6 +791,7 @@ static int dispatch_block16r(const PlanR& p, int SP, const Block16RArgs& a, hipS
   if (SP == 1) {
     if (p.NT == 1 && p.MT == 4) return launch_block16r<1, 4, 1>(a, st);
     if (p.NT == 2 && p.MT == 4) return launch_block16r<2, 4, 1>(a, st);
+    if (p.NT == 3 && p.MT == 3) return launch_block16r<3, 3, 1>(a, st);
   } else {
     if (p.NT == 1 && p.MT == 4 * X) return launch_block16r<1, 4 * X, 2>(a, st);
     if (p.NT == 2 && p.MT == 2 * X) return launch_block16r<2, 2 * X, 2>(a, st);
