@@ -499,6 +499,9 @@ __global__ void pack_conv2x3_kernel(const float* __restrict__ w, __bf16* __restr
 //   the lane with member 0 stores 4 channels' hi and lo runs (8 B each).
 // ---------------------------------------------------------------------------- //
 constexpr int C1X3_KH = 20, C1X3_KW = 8, C1X3_COLS = 32, C1X3_HMAX = 101;
+#ifndef HONK_C1_PREFETCH  // load the next clip's rows during this clip's MFMAs
+#define HONK_C1_PREFETCH 0  // measured 0.4% slower with it on (15 VGPR spills)
+#endif
 constexpr int C1X3_PLANE = C1X3_HMAX * C1X3_COLS * 16;  // bytes of one (hi or lo) plane
 
 struct Conv1X3Args {
@@ -593,15 +596,33 @@ __global__ __launch_bounds__(512, 1) void conv1x3_kernel(Conv1X3Args a) {
     }
   };
 
-  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+  // the next clip's raw rows are loaded into registers while this clip computes
+  // (NE entries of 8 floats per thread), converted and written at its start
+  constexpr int NE = (C1X3_HMAX * C1X3_COLS + 511) / 512;
+  f32x4 pu[NE], pv[NE];
+  auto fetch = [&](int bb) {
+    const bool ok = bb < a.B;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.x + (size_t)b * clip_floats), (short)0, clip_floats * 4, 0x00020000);
-    __syncthreads();  // every wave is done with the previous clip's image
-    for (int e = tid; e < entries; e += 512) {
+        (void*)(a.x + (size_t)(ok ? bb : 0) * clip_floats), (short)0, ok ? clip_floats * 4 : 0, 0x00020000);
+#pragma unroll
+    for (int n = 0; n < NE; ++n) {
+      const int e = tid + n * 512;
       const int r = e / C1X3_COLS, c = e - r * C1X3_COLS;
-      const int o = (r * a.W + c) * 4;
-      const f32x4 u = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
-      const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, 0, 0));
+      const int o = e < entries ? (r * a.W + c) * 4 : 0x40000000;
+      pu[n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+      pv[n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, 0, 0));
+    }
+  };
+  if constexpr (HONK_C1_PREFETCH) fetch(blockIdx.x);
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    __syncthreads();  // every wave is done with the previous clip's image
+    if constexpr (!HONK_C1_PREFETCH) fetch(b);
+#pragma unroll
+    for (int n = 0; n < NE; ++n) {
+      const int e = tid + n * 512;
+      if (e >= entries) break;
+      const int r = e / C1X3_COLS, c = e - r * C1X3_COLS;
+      const f32x4 u = pu[n], v = pv[n];
       cbf16x8 h, l;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -614,6 +635,7 @@ __global__ __launch_bounds__(512, 1) void conv1x3_kernel(Conv1X3Args a) {
       *(cbf16x8*)(img + C1X3_PLANE + slot) = l;
     }
     __syncthreads();
+    if constexpr (HONK_C1_PREFETCH) fetch(b + gridDim.x);
     __bf16* ob = a.out + (size_t)b * a.PH * a.PW * 128;
     AFr A0, A1;
     int mt = mg;
