@@ -314,8 +314,16 @@ def main():
     dist = world > 1
     if dist:
         import torch.distributed as tdist
+        # rehearsal knobs for a 1-GPU box (never set by the driver): HONK_BENCH_BACKEND=gloo
+        # and HONK_BENCH_ONE_GPU=1 run N ranks on cuda:0 over gloo; the real N-GPU run is RCCL
+        if os.environ.get("HONK_BENCH_ONE_GPU"):
+            local = 0
+        backend = os.environ.get("HONK_BENCH_BACKEND", "nccl")
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 

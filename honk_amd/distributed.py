@@ -63,6 +63,8 @@ def max_over_ranks(value: float, device=None) -> float:
     rank, world = _ctx()
     if world == 1:
         return value
+    if dist.get_backend() == "gloo":
+        device = None  # gloo reduces host tensors
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
