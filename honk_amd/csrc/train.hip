@@ -67,7 +67,11 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
 // rows of every channel are staged in LDS once; each thread owns NP output
 // pixels x all C outputs (weights read as LDS broadcasts, 4 per ds_read_b128).
 // ---------------------------------------------------------------------------- //
-constexpr int TC_XL = 64 * 1024;  // bytes of the staged input tile
+constexpr int TC_XL = 64 * 1024;  // bytes of the staged input tile (wgrad: and of its dy tile)
+#ifndef HONK_TC_XLC
+#define HONK_TC_XLC (64 * 1024)
+#endif
+constexpr int TC_XLC = HONK_TC_XLC;  // conv3x3_kernel's input tile (19 maps); 96 KB = whole clips, 4 px/thread, 1 block/CU: 23 % slower step
 
 template <int C>
 struct TC {
@@ -88,7 +92,7 @@ template <int C, int NP>
 __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
   constexpr int CW = TC<C>::CW;
   __shared__ __attribute__((aligned(16))) float wl[TC<C>::WL];
-  __shared__ __attribute__((aligned(16))) float xl[TC_XL / 4];
+  __shared__ __attribute__((aligned(16))) float xl[(C <= 20 ? TC_XLC : TC_XL) / 4];
   const int tid = threadIdx.x;
   for (int i = tid; i < TC<C>::WL; i += 256) {
     const int o = i % CW, it = i / CW, in = it / 9, t = it - in * 9;
@@ -407,12 +411,14 @@ static int bn_slices(int B, int C) {
 
 // rows per tile: the staged input (C planes of (TH+2) x (W+2)) and (wgrad) its dy
 // within TC_XL, at most 1024 pixels (4 per thread); bands balanced over the clip
-static int tc_rows(int C, int H, int W) {
-  int th = TC_XL / 4 / (C * (W + 2)) - 2;
+static int tc_rows(int C, int H, int W, bool conv = false) {
+  int th = (conv && C <= 20 ? TC_XLC : TC_XL) / 4 / (C * (W + 2)) - 2;
   const int byp = (C <= 20 ? 1024 : 512) / W;  // conv3x3_kernel: NP <= 4 (19 maps) / 2 (45 maps)
   if (th > byp) th = byp;
-  const int byd = TC_XL / 4 / (((C + 3) & ~3) * W);
-  if (th > byd) th = byd;
+  if (!conv) {
+    const int byd = TC_XL / 4 / (((C + 3) & ~3) * W);
+    if (th > byd) th = byd;
+  }
   if (th > H) th = H;
   if (th < 1) return 0;
   const int nb = (H + th - 1) / th;
@@ -446,7 +452,7 @@ int tc_check(const void* a, const void* b, const void* c, int64_t batch, int32_t
   if (!a || !b || !c) return fail(HONK_ERR_ARG, "null pointer argument");
   if (batch < 0 || h < 1 || w < 1) return fail(HONK_ERR_ARG, "bad conv3x3 shape (B=%lld H=%d W=%d)", (long long)batch, h, w);
   if (ch != 19 && ch != 45) return fail(HONK_ERR_UNSUPPORTED, "conv3x3 training kernels: C=%d (19 or 45)", ch);
-  if (train::tc_rows(ch, h, w) < 1) return fail(HONK_ERR_UNSUPPORTED, "conv3x3: width %d too large", w);
+  if (train::tc_rows(ch, h, w) < 1 || train::tc_rows(ch, h, w, true) < 1) return fail(HONK_ERR_UNSUPPORTED, "conv3x3: width %d too large", w);
   if (batch * (int64_t)h > 0x3fffffff) return fail(HONK_ERR_ARG, "conv3x3: batch too large");
   return HONK_OK;
 }
@@ -460,7 +466,7 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   train::Conv3Args a;
   a.x = x; a.w = w; a.y = y;
   a.B = (int)batch; a.H = h; a.W = w_; a.flip = flip ? 1 : 0;
-  a.TH = train::tc_rows(c, h, w_);
+  a.TH = train::tc_rows(c, h, w_, true);
   a.nband = (h + a.TH - 1) / a.TH;
   const int grid = train::tc_grid((int64_t)a.B * a.nband);
   hipStream_t st = (hipStream_t)stream;
