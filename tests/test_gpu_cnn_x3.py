@@ -80,3 +80,15 @@ def test_cnn_x3_conv2_fast_path_multi_clip_per_block(monkeypatch):
     monkeypatch.setenv("HONK_CNN_C2X3", "0")  # generic GEMMs for both convs
     gen = run(m, x)
     np.testing.assert_allclose(fast, gen, atol=ATOL, rtol=0)
+
+
+@pytest.mark.parametrize("B", [1, 2, 257])
+def test_cnn_x3_fast_path_batch_edges(B):
+    # conv1x3 / conv2x3 grids are min(B, CUs) persistent workgroups: a single clip,
+    # two clips, and one clip past a 256-CU grid
+    name = "cnn-trad-pool2"
+    cfg = dict(ref_configs()[name])
+    params = orc.make_params(cfg, 11 + B)
+    x = np.random.Generator(np.random.PCG64(B)).standard_normal((B, 101, 40)).astype(np.float32)
+    out = run(module(cfg, params, name), x)
+    np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=ATOL, rtol=0)

@@ -108,3 +108,20 @@ def test_train_step_grads_match_pytorch(name, B, bar):
         en, et = _rel(gn[k], g64[k]), _rel(gt[k], g64[k])
         print(f"{name} {k}: native {en:.2e}  pytorch-fp32 {et:.2e}")
         assert en <= max(et, bar), (k, en, et)
+
+
+def test_native_train_minimum_batch_and_eval_switch():
+    # B = 2 (BatchNorm's minimum in training), then eval on the native forward path
+    torch.manual_seed(3)
+    cfg = dict(hm.find_config("res8-narrow"))
+    m = hm.find_model("res8-narrow")(cfg).to(DEV).train()
+    x = torch.randn(2, 101, 40, device=DEV)
+    loss = m(x).square().mean()
+    loss.backward()
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+    assert int(m.bn1.num_batches_tracked) == 1
+    m.eval()
+    with torch.no_grad():
+        gpu = m(x).cpu()
+        cpu = m.cpu()(x.cpu())
+    torch.testing.assert_close(gpu, cpu, rtol=0, atol=1e-4)
