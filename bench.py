@@ -88,7 +88,10 @@ def cpu_baseline(cfg, seconds):
 
 
 def cfg_name(cfg):
-    return f"res{cfg['n_layers']}-{cfg['n_feature_maps']}maps" if "n_layers" in cfg else "cnn"
+    if "n_layers" not in cfg:
+        return "cnn"
+    return (f"res (n_layers {cfg['n_layers']}, {cfg['n_feature_maps']} maps"
+            f"{', dilated' if cfg.get('use_dilation') else ''})")
 
 
 def load_traffic(kernel, clips_per_launch, model):
