@@ -4,13 +4,22 @@
     python bench.py [--gpus N --steps K --warmup W --batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
+``--gpus N`` without a torchrun environment: this process never touches the GPU;
+it starts N rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one
+GPU each, RCCL) and exits with their status.  Only rank 0 prints.
+
 One step = one forward of B clips per GPU (weak scaling: per-GPU batch fixed;
 the batch shards across ranks with no collective on the data path).  Prints ONE
-JSON line on rank 0 (see DESIGN.md "Measurement").
+JSON line on rank 0 (see DESIGN.md "Measurement").  Besides the headline
+(res15, bf16x3) the line carries the other res15 precision modes and the
+BASELINE.json configs C2 (cnn-trad-pool2 fp32 + bf16x3), C3 (res8 bf16) and C5
+(res26-narrow training, DP over RCCL), each with its roofline.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,14 +33,23 @@ METRIC = "1s-clips/sec (whole node) + top-1 acc, res15 12-label Speech Commands"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak (= FP32 vector peak)
 HBM_PEAK_GBS = 8000.0
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
+# MFMA peak per precision mode in ALGORITHMIC flop: bf16x3 spends 3 bf16 products per MAC
+MODE_PEAK = {"f32": FP32_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3, "bf16": BF16_MFMA_PEAK_TFLOPS}
 WORKLOADS = {
     "res15": "res15 eval forward (SpeechResModel, 13 dilated 3x3 res layers, 45 maps, 12 labels)",
     "res8": "res8 eval forward (SpeechResModel, avg-pool 4x3, 6 res layers, 45 maps, 12 labels)",
     "cnn-trad-pool2": "cnn-trad-pool2 eval forward (SpeechModel, conv 20x8 + maxpool 2x2 + conv 10x4 + linear, 4 labels)",
 }
+PREC_NOTES = {
+    "bf16x3": "fp32 values carried as bf16 (hi, lo) pairs; products hi*hi + hi*lo + lo*hi on bf16 MFMA, fp32 "
+              "accumulation; meets the fp32 1e-4 logit parity bar (tests/test_gpu_bf16x3.py)",
+    "f32": "IEEE fp32 on v_mfma_f32_16x16x4_f32; 1e-4 logit parity",
+    "bf16": "bf16 activations/weights, fp32 accumulation; top-1 parity only (reduced precision vs the fp32 "
+            "reference), so never the headline",
+}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
@@ -45,23 +63,124 @@ def parse():
                    help="res path arithmetic: bf16x3 (fp32 values as bf16 hi/lo pairs, 3 bf16 MFMA products, "
                         "fp32 accumulation; 1e-4 parity), f32 (fp32 MFMA; 1e-4 parity) or bf16 (top-1 parity)")
     p.add_argument("--no-alt", action="store_true",
-                   help="skip the extra measurements of the other res precision modes")
+                   help="skip the extra measurements (other precision modes, C2, C3, C5)")
     p.add_argument("--e2e", action="store_true",
                    help="serving pipeline: int16-scaled PCM [B,16000] in HBM -> GPU MFCC -> model -> logits")
     p.add_argument("--train", action="store_true",
-                   help="C5: data-parallel training step (fwd+bwd, one RCCL all-reduce, fused SGD)")
-    return p.parse_args()
+                   help="only C5: data-parallel training step (fwd+bwd, one RCCL all-reduce, fused SGD)")
+    return p.parse_args(argv)
+
+
+def log(msg):
+    """Progress on stderr (stdout carries exactly one JSON line)."""
+    print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# --gpus N launcher: the parent never initialises HIP
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_envs(n, port, base=None):
+    """Environment of each rank process for a single-node N-GPU run (torchrun's variables)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def _route(stream, is_rank0):
+    """Forward a rank's stdout: rank 0's JSON result line to our stdout, everything
+    else (library chatter such as gloo's connection lines) to stderr."""
+    for line in iter(stream.readline, ""):
+        if is_rank0 and line.lstrip().startswith("{"):
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    stream.close()
+
+
+def spawn_ranks(n, argv, script=None):
+    """Start n rank processes of this script and wait for them; returns the exit status.
+
+    A rank that fails ends the others (they would otherwise wait in a collective).
+    Called before anything touches the GPU (torch.cuda.device_count() does not
+    initialise HIP on this image)."""
+    import threading
+    if not os.environ.get("HONK_BENCH_ONE_GPU"):
+        have = torch.cuda.device_count()
+        if have < n:
+            log(f"--gpus {n} but only {have} visible GPU(s)")
+            return 2
+    script = script or os.path.abspath(__file__)
+    procs, pumps = [], []
+    for r, e in enumerate(rank_envs(n, _free_port())):
+        p = subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e, stdout=subprocess.PIPE, text=True)
+        t = threading.Thread(target=_route, args=(p.stdout, r == 0), daemon=True)
+        t.start()
+        procs.append(p)
+        pumps.append(t)
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            r = p.poll()
+            if r is None:
+                continue
+            alive.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.1)
+    for t in pumps:
+        t.join(timeout=10)
+    return rc
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU baseline
+# ---------------------------------------------------------------------------------------------
+def cpu_share():
+    """Host threads this process may use: the CPU affinity mask, capped by a cgroup
+    cpu.max quota and by OMP_NUM_THREADS when set (16 on the GPU pool, whose
+    os.cpu_count() shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):  # pragma: no cover
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(float(q) / float(per))))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    if omp > 0:
+        n = min(n, omp)
+    return max(1, n)
 
 
 def cpu_baseline(cfg, seconds):
     """The reference's CPU path restated (oracle/ref_torch.py: stock torch fp32 eval
-    forward, what utils/train.py --no_cuda runs) on the host cores: bounded sample.
-    Threads = the box's CPU share (16 on the GPU pool; os.cpu_count() shows the
-    whole machine there), batches as SURVEY.md §8(d): 64 clips for res15, else 256."""
-    import torch
+    forward, what utils/train.py --no_cuda runs) on the host cores: bounded sample,
+    batches as SURVEY.md §8(d): 64 clips for res15, else 256."""
     from oracle import ref_numpy as orc
     from oracle import ref_torch
-    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    cores = cpu_share()
     torch.set_num_threads(cores)
     params = ref_torch.tensors(orc.make_params(cfg, 0))
     rng = np.random.Generator(np.random.PCG64(1))
@@ -84,7 +203,8 @@ def cpu_baseline(cfg, seconds):
     return {"value": n / dt, "unit": "clips/s", "cores": int(cores), "kind": "port",
             "sample": f"{n} clips of {cfg_name(cfg)} in {dt:.1f} s (oracle/ref_torch.py: torch {torch.__version__} "
                       f"CPU fp32 eval forward, batches of {per}, {cores} threads)",
-            "cpu_model": model_name, "os_cpu_count": os.cpu_count()}
+            "cpu_model": model_name, "os_cpu_count": os.cpu_count(),
+            "threads_source": "sched_getaffinity / cgroup cpu.max / OMP_NUM_THREADS"}
 
 
 def cfg_name(cfg):
@@ -94,6 +214,9 @@ def cfg_name(cfg):
             f"{', dilated' if cfg.get('use_dilation') else ''})")
 
 
+# ---------------------------------------------------------------------------------------------
+# rooflines
+# ---------------------------------------------------------------------------------------------
 def load_traffic(kernel, clips_per_launch, model):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC pass
     (profiles/pmc_<kernel>.json, written by tools/pmc_summary.py), or None when no
@@ -111,23 +234,190 @@ def load_traffic(kernel, clips_per_launch, model):
     return d.get("hbm_bytes_per_launch")
 
 
-def train_bench(args, dev, rank, world, barrier):
-    """C5: res26-narrow train step per rank (fwd+bwd on device, flat-bucket all-reduce, fused SGD)."""
-    from honk_amd import distributed as hd
+def _res_geometry(cfg):
+    """(H, W, n_layers, CP) of a res config's block layers (model.py:87-98)."""
+    ph, pw = tuple(cfg.get("res_pool", (1, 1)))
+    C = int(cfg["n_feature_maps"])
+    return 101 // ph, 40 // pw, int(cfg["n_layers"]), 16 * ((C + 15) // 16)
+
+
+def res_roofline(prec, cfg, kms, nl, kfl, B, model):
+    """Roofline of the dominant res kernel (the dilated 3x3 block conv) for a precision mode.
+
+    MFMA-bound: achieved = ALGORITHMIC flop per launch (2 x 9 x C^2 x
+    H x W per clip-layer x clips per launch, no padding, one product per MAC) / the
+    mean launch time (HIP events on the launch stream); peak = the MFMA peak of the
+    mode in algorithmic flop (fp32 157.3 TF; bf16x3 = bf16 2.5 PF / 3 products;
+    bf16 2.5 PF).  Beside it: the kernel's algorithmic activation bytes as an HBM
+    rate, and the PMC-measured HBM traffic per launch."""
+    avg_s = (kms / max(nl, 1)) * 1e-3
+    clips = min(B, 4096)
+    fl = kfl / max(nl, 1)
+    ach = fl / avg_s / 1e12 if nl else None
+    peak = MODE_PEAK[prec]
+    H, W, L, CP = _res_geometry(cfg)
+    if prec == "f32":
+        fam, kname = "block_kernel", "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)"
+        traffic = load_traffic("block_kernel", clips, model)
+        act = H * W * CP * 4
+    else:
+        sp = 2 if prec == "bf16x3" else 1
+        fam = "block16_kernel" if os.environ.get("HONK_RES_ROWBAND") == "0" else "block16r_kernel"
+        kname = f"honk::res::{fam}<..., SP={sp}> (dilated 3x3 conv, bf16 MFMA{', 3 products' if sp == 2 else ''})"
+        traffic = load_traffic(f"{fam}_sp{sp}", clips, model)
+        act = H * W * CP * 2 * sp
+    # per clip-layer activation bytes the layer-by-layer schedule moves (read X [+R], write Y)
+    per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1)) / L
+    bw = per_clip * clips / avg_s / 1e9 if nl else None
+    out = {"bound": "mfma", "kernel": kname,
+           "achieved": round(ach, 2) if ach else None, "peak": round(peak, 1), "unit": "TFLOP/s",
+           "frac": round(ach / peak, 4) if ach else None,
+           "traffic": traffic,
+           "launches": nl, "avg_launch_ms": round(kms / max(nl, 1), 4), "clips_per_launch": clips,
+           "flop_per_launch": fl,
+           "flop_def": "algorithmic: 2*9*C^2*H*W per clip-layer (SURVEY §8(d)), no channel/tile padding",
+           "hbm": {"activation_bytes_per_launch": per_clip * clips,
+                   "achieved_GBs": round(bw, 1) if bw else None, "peak_GBs": HBM_PEAK_GBS,
+                   "frac": round(bw / HBM_PEAK_GBS, 4) if bw else None}}
+    if prec == "bf16x3" and ach:
+        out["frac_of_raw_bf16_peak"] = round(ach / BF16_MFMA_PEAK_TFLOPS, 4)
+    return out
+
+
+def _sample_parity(model, cfg, x, out, orc, B):
+    idx = list(range(0, B, max(1, B // 32)))[:32]
+    ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}, cfg,
+                      x[idx].cpu().numpy())
+    got = out[idx].cpu().numpy()
+    return {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
+            "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()),
+            "sample_clips": len(idx)}
+
+
+class Ctx:
+    """What every measurement needs: device, ranks, barrier, native handle."""
+
+    def __init__(self, dev, rank, world, dist):
+        from honk_amd import _native
+        from honk_amd import distributed as hd
+        self.dev, self.rank, self.world, self.dist = dev, rank, world, dist
+        self.native, self.hd = _native, hd
+
+    def barrier(self):
+        if self.dist:
+            import torch.distributed as tdist
+            tdist.barrier()
+
+    def timed(self, fn, x, steps, warmup):
+        """Run warmup + steps of fn(x) between barriers; returns (max-over-ranks seconds,
+        per-rank seconds, last output, (kernel ms, launches, flop))."""
+        with torch.no_grad():
+            for _ in range(warmup):
+                fn(x)
+            torch.cuda.synchronize()
+            self.barrier()
+            torch.cuda.synchronize()
+            self.native.timing_enable(True)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                out = fn(x)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            self.barrier()
+            k = self.native.timing_read()
+            self.native.timing_enable(False)
+        per = self.hd.gather_scalar(t1 - t0, device=self.dev)
+        return max(per), per, out, k
+
+
+def measure_res(ctx, args, name, prec, B, x=None, model=None):
+    """A res model's eval forward of B clips per GPU in one precision mode."""
     from honk_amd import model as hm
-    from honk_amd.optim import FlatParams, FlatSGD
-    name = args.model if args.model != "res15" else "res26-narrow"
-    B = args.batch or 4096
+    from oracle import ref_numpy as orc
+    cfg = dict(hm.find_config(name))
+    if model is None:
+        torch.manual_seed(0)
+        model = hm.find_model(name)(cfg).eval().to(ctx.dev)
+    if x is None:
+        g = torch.Generator(device=ctx.dev).manual_seed(1234 + ctx.rank)
+        x = torch.randn(B, 101, 40, device=ctx.dev, generator=g)
+    keep = getattr(model, "honk_precision", "f32")
+    model.honk_precision = prec
+    el, per, out, (kms, nl, kfl) = ctx.timed(model, x, args.steps, max(1, args.warmup))
+    model.honk_precision = keep
+    return {"value": round(ctx.world * B * args.steps / el, 1), "unit": "clips/s", "dtype": prec,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "per_rank_clips_s": [round(B * args.steps / t, 1) for t in per],
+            "roofline": res_roofline(prec, cfg, kms, nl, kfl, B, name),
+            "parity": _sample_parity(model, cfg, x, out, orc, B),
+            "note": PREC_NOTES[prec]}
+
+
+def measure_c2(ctx, args):
+    """Config C2 (BASELINE.json configs[1]): cnn-trad-pool2 eval forward, 65,536
+    clips per GPU, in fp32 (the config as named) and bf16x3 (1e-4 parity).
+    Roofline: algorithmic conv FLOP per launch over the conv kernels' mean launch
+    time (HIP events on the launch stream), vs the fp32 MFMA peak (resp. bf16 peak / 3)."""
+    from honk_amd import model as hm
+    from oracle import ref_numpy as orc
+    name = "cnn-trad-pool2"
     cfg = dict(hm.find_config(name))
     torch.manual_seed(0)
-    model = hm.find_model(name)(cfg).to(dev).train()
+    model = hm.find_model(name)(cfg).eval().to(ctx.dev)
+    B = 65536
+    g = torch.Generator(device=ctx.dev).manual_seed(4321 + ctx.rank)
+    x = torch.randn(B, 101, 40, device=ctx.dev, generator=g)
+    out = {"workload": "cnn-trad-pool2 eval forward (config C2), 65,536 clips per GPU", "per_gpu_batch": B}
+    for prec in ("f32", "bf16x3"):
+        model.honk_precision = prec
+        el, per, y, (kms, nl, kfl) = ctx.timed(model, x, args.steps, max(1, args.warmup))
+        peak = MODE_PEAK[prec]
+        ach = (kfl / max(nl, 1)) / (kms / max(nl, 1) * 1e-3) / 1e12 if nl else None
+        out[f"{prec}_mode"] = {
+            "value": round(ctx.world * B * args.steps / el, 1), "unit": "clips/s", "dtype": prec,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "per_rank_clips_s": [round(B * args.steps / t, 1) for t in per],
+            "roofline": {"bound": "mfma",
+                         "kernel": ("honk::cnn::conv1x3_kernel + conv2x3_kernel (bf16x3 convs, 3 bf16 MFMA "
+                                    "products per MAC; peak = bf16 peak / 3)" if prec == "bf16x3" else
+                                    "honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM convs, fp32 MFMA)"),
+                         "achieved": round(ach, 2) if ach else None, "peak": round(peak, 1), "unit": "TFLOP/s",
+                         "frac": round(ach / peak, 4) if ach else None, "launches": nl,
+                         "avg_launch_ms": round(kms / max(nl, 1), 4), "flop_per_launch": kfl / max(nl, 1),
+                         "traffic": None},
+            "parity": _sample_parity(model, cfg, x, y, orc, B),
+            "note": PREC_NOTES.get(prec, "")}
+    del x
+    return out
+
+
+def train_flops_per_clip(cfg):
+    """Algorithmic training FLOP per clip: forward + input grad (every layer but conv0)
+    + weight grad, each 2 x MACs (~3x forward - conv0 dgrad)."""
+    from oracle import ref_numpy as orc
+    fwd = orc.flops_per_clip(cfg)
+    conv0 = 2 * 101 * 40 * int(cfg["n_feature_maps"]) * 9
+    return 3 * fwd - conv0
+
+
+def measure_train(ctx, args, name="res26-narrow", B=None):
+    """C5: res26-narrow train step per rank (fwd+bwd on device, flat-bucket all-reduce
+    over RCCL when world > 1, fused SGD).  Roofline: algorithmic training FLOP per
+    step / step time vs the fp32 peak (the native training convs are fp32)."""
+    from honk_amd import model as hm
+    from honk_amd.optim import FlatParams, FlatSGD
+    hd = ctx.hd
+    B = B or 4096
+    cfg = dict(hm.find_config(name))
+    torch.manual_seed(0)
+    model = hm.find_model(name)(cfg).to(ctx.dev).train()
     hd.broadcast_module(model)
     flat = FlatParams(model)
     opt = FlatSGD(flat, lr=0.1, momentum=0.9, weight_decay=1e-5)
     crit = torch.nn.CrossEntropyLoss()
-    g = torch.Generator(device=dev).manual_seed(99 + rank)
-    x = torch.randn(B, 101, 40, device=dev, generator=g)
-    y = torch.randint(0, cfg["n_labels"], (B,), device=dev, generator=g)
+    g = torch.Generator(device=ctx.dev).manual_seed(99 + ctx.rank)
+    x = torch.randn(B, 101, 40, device=ctx.dev, generator=g)
+    y = torch.randint(0, cfg["n_labels"], (B,), device=ctx.dev, generator=g)
 
     def step():
         opt.zero_grad()
@@ -137,180 +427,40 @@ def train_bench(args, dev, rank, world, barrier):
         opt.step(grad_scale=hd.allreduce_grads(flat))
         return loss
 
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
-    barrier()
+    ctx.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    barrier()
-    elapsed = hd.max_over_ranks(t1 - t0, device=dev)
-    value = world * B * args.steps / elapsed
-    if rank == 0:
-        print(json.dumps({
-            "metric": "train clips/sec (whole node), res26-narrow fwd+bwd+SGD, DP over RCCL (config C5)",
-            "value": round(value, 1), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic N(0,1) [B,101,40] inputs + uniform labels resident in HBM",
-            "config": {"workload": f"{name} training step (train mode BN batch stats, CE loss, SGD m=0.9)",
-                       "per_gpu_batch": B, "global_batch": world * B,
-                       "parallelism": f"dp{world}: one flat fp32 grad bucket all-reduce ({flat.numel} params)"},
-            "final_loss": float(loss.item()),
-            "roofline": None,
-            "note": "native kernels: the block convs' forward / input grad / weight grad "
-                    "(honk_conv3x3_f32, honk_conv3x3_wgrad_f32), train-mode BatchNorm fwd/bwd "
-                    "(honk_bn_train_*), fused SGD over the flat all-reduced bucket; conv0, pooling, ReLU, "
-                    "residual, mean, Linear and the loss run on PyTorch autograd on the device"}),
-              flush=True)
+    ctx.barrier()
+    per = hd.gather_scalar(t1 - t0, device=ctx.dev)
+    el = max(per)
+    fl = train_flops_per_clip(cfg)
+    ach = B * args.steps * fl / el / 1e12
+    return {
+        "metric": "train clips/sec (whole node), res26-narrow fwd+bwd+SGD, DP over RCCL (config C5)",
+        "value": round(ctx.world * B * args.steps / el, 1), "unit": "clips/s", "dtype": "f32",
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "per_rank_clips_s": [round(B * args.steps / t, 1) for t in per],
+        "config": {"workload": f"{name} training step (train-mode BN batch stats, CE loss, SGD m=0.9, wd 1e-5)",
+                   "per_gpu_batch": B, "global_batch": ctx.world * B,
+                   "parallelism": f"dp{ctx.world}: one flat fp32 grad bucket all-reduce ({flat.numel} params)"},
+        "final_loss": float(loss.item()),
+        "roofline": {"bound": "mfma", "kernel": "whole training step (per-GPU)",
+                     "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "flop_per_clip": fl,
+                     "flop_def": "2 x (forward + input-grad + weight-grad MACs), conv0 has no input grad"},
+        "note": "native kernels: the block convs' forward / input grad / weight grad, train-mode BatchNorm "
+                "fwd/bwd, fused SGD over the flat all-reduced bucket; conv0, pooling, ReLU, residual, mean, "
+                "Linear and the loss run on PyTorch autograd on the device"}
 
 
-def _res_geometry(cfg):
-    """(H, W, n_layers, CP) of a res config's block layers (model.py:87-98)."""
-    ph, pw = tuple(cfg.get("res_pool", (1, 1)))
-    C = int(cfg["n_feature_maps"])
-    return 101 // ph, 40 // pw, int(cfg["n_layers"]), 16 * ((C + 15) // 16)
-
-
-PREC_NOTES = {
-    "bf16x3": "fp32 values carried as bf16 (hi, lo) pairs; products hi*hi + hi*lo + lo*hi on bf16 MFMA, fp32 "
-              "accumulation; meets the fp32 1e-4 logit parity bar (tests/test_gpu_bf16x3.py)",
-    "f32": "IEEE fp32 on v_mfma_f32_16x16x4_f32; 1e-4 logit parity",
-    "bf16": "bf16 activations/weights, fp32 accumulation; top-1 parity only (reduced precision vs the fp32 "
-            "reference), so never the headline",
-}
-
-
-def res_roofline(prec, cfg, kms, nl, kfl, B, model):
-    """Roofline of the dominant res kernel for a precision mode.
-
-    f32: MFMA-bound -- algorithmic FLOP per launch / mean launch time vs the fp32
-    MFMA peak.  bf16 / bf16x3 (block16_kernel, SP = 1 / 2): HBM-bound --
-    algorithmic bytes per launch = clips x (read X [+ read residual on even layers]
-    [+ write Y except the last layer]) x H*W*CP*2*SP, averaged over the layers of
-    one forward, / the mean launch time."""
-    avg_s = (kms / max(nl, 1)) * 1e-3
-    clips = min(B, 4096)
-    if prec == "f32":
-        ach = (kfl / max(nl, 1)) / avg_s / 1e12 if nl else None
-        return {"bound": "mfma", "kernel": "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)",
-                "achieved": round(ach, 2) if ach else None, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None,
-                "traffic": load_traffic("block_kernel", clips, model),
-                "launches": nl, "avg_launch_ms": round(kms / max(nl, 1), 4),
-                "flop_per_launch": kfl / max(nl, 1)}
-    sp = 2 if prec == "bf16x3" else 1
-    H, W, L, CP = _res_geometry(cfg)
-    act = H * W * CP * 2 * sp
-    per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1)) / L
-    bw = per_clip * clips / avg_s / 1e9 if nl else None
-    mf = (kfl * (3 if sp == 2 else 1) / max(nl, 1)) / avg_s / 1e12 if nl else None
-    # every res config runs the row-band kernel (HONK_RES_ROWBAND=0: the per-dy-stage one)
-    fam = "block16_kernel" if os.environ.get("HONK_RES_ROWBAND") == "0" else "block16r_kernel"
-    return {"bound": "hbm", "kernel": f"honk::res::{fam}<..., SP={sp}> (dilated 3x3 conv, bf16 MFMA)",
-            "achieved": round(bw, 1) if bw else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(bw / HBM_PEAK_GBS, 4) if bw else None,
-            "traffic": load_traffic(f"{fam}_sp{sp}", clips, model),
-            "launches": nl, "avg_launch_ms": round(kms / max(nl, 1), 4),
-            "algorithmic_bytes_per_launch": per_clip * clips,
-            "mfma": {"executed_bf16_tflops": round(mf, 2) if mf else None, "peak": BF16_MFMA_PEAK_TFLOPS,
-                     "frac": round(mf / BF16_MFMA_PEAK_TFLOPS, 4) if mf else None}}
-
-
-def measure_mode(prec, model, x, args, dev, barrier, hd, _native, orc, cfg, B, world):
-    """The same res workload in another precision mode (reported beside the headline)."""
-    keep = model.honk_precision
-    model.honk_precision = prec
-    with torch.no_grad():
-        for _ in range(max(1, args.warmup)):
-            model(x)
-        torch.cuda.synchronize()
-        barrier()
-        _native.timing_enable(True)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = model(x)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        barrier()
-        kms, nl, kfl = _native.timing_read()
-        _native.timing_enable(False)
-    model.honk_precision = keep
-    el = hd.max_over_ranks(t1 - t0, device=dev)
-    idx = list(range(0, B, max(1, B // 32)))[:32]
-    ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}, cfg,
-                      x[idx].cpu().numpy())
-    got = out[idx].cpu().numpy()
-    return {"value": round(world * B * args.steps / el, 1), "unit": "clips/s", "dtype": prec,
-            "ms_per_step": round(el / args.steps * 1e3, 3),
-            "roofline": res_roofline(prec, cfg, kms, nl, kfl, B, args.model),
-            "parity": {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
-                       "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()),
-                       "sample_clips": len(idx)},
-            "note": PREC_NOTES[prec]}
-
-
-def measure_c2(args, dev, barrier, hd, _native, orc, world, rank):
-    """Config C2 (BASELINE.json configs[1]): cnn-trad-pool2 eval forward, 65,536
-    clips per GPU, in bf16x3 (1e-4 parity) and fp32 MFMA, reported beside the res15
-    headline.  Roofline: algorithmic conv FLOP per launch over the conv kernels'
-    mean launch time (HIP events on the launch stream), vs bf16 peak / 3 (bf16x3)
-    or the fp32 MFMA peak."""
-    from honk_amd import model as hm
-    name = "cnn-trad-pool2"
-    cfg = dict(hm.find_config(name))
-    torch.manual_seed(0)
-    model = hm.find_model(name)(cfg).eval().to(dev)
-    B = 65536
-    g = torch.Generator(device=dev).manual_seed(4321 + rank)
-    x = torch.randn(B, 101, 40, device=dev, generator=g)
-    out = {"workload": "cnn-trad-pool2 eval forward (config C2), 65,536 clips per GPU", "per_gpu_batch": B}
-    for prec in ("bf16x3", "f32"):
-        model.honk_precision = prec
-        with torch.no_grad():
-            for _ in range(max(1, args.warmup)):
-                model(x)
-            torch.cuda.synchronize()
-            barrier()
-            _native.timing_enable(True)
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                y = model(x)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            barrier()
-            kms, nl, kfl = _native.timing_read()
-            _native.timing_enable(False)
-        el = hd.max_over_ranks(t1 - t0, device=dev)
-        idx = list(range(0, B, B // 32))[:32]
-        ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}, cfg,
-                          x[idx].cpu().numpy())
-        got = y[idx].cpu().numpy()
-        peak = FP32_MFMA_PEAK_TFLOPS if prec == "f32" else BF16_MFMA_PEAK_TFLOPS / 3
-        ach = (kfl / max(nl, 1)) / (kms / max(nl, 1) * 1e-3) / 1e12 if nl else None
-        out[f"{prec}_mode"] = {
-            "value": round(world * B * args.steps / el, 1), "unit": "clips/s", "dtype": prec,
-            "ms_per_step": round(el / args.steps * 1e3, 3),
-            "roofline": {"bound": "mfma",
-                         "kernel": ("honk::cnn::conv1x3_kernel + conv2x3_kernel (bf16x3 convs, 3 bf16 MFMA "
-                                    "products per MAC; peak = bf16 peak / 3)" if prec == "bf16x3" else
-                                    "honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM convs, fp32 MFMA)"),
-                         "achieved": round(ach, 2) if ach else None, "peak": round(peak, 1), "unit": "TFLOP/s",
-                         "frac": round(ach / peak, 4) if ach else None, "launches": nl,
-                         "avg_launch_ms": round(kms / max(nl, 1), 4), "flop_per_launch": kfl / max(nl, 1)},
-            "parity": {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
-                       "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()),
-                       "sample_clips": len(idx)},
-            "note": PREC_NOTES.get(prec, "")}
-    del x
-    return out
-
-
-def main():
-    args = parse()
+def rank_main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -329,88 +479,90 @@ def main():
             tdist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-
-    from honk_amd import _native
-    from honk_amd import distributed as hd
-    from honk_amd import model as hm
-    from oracle import ref_numpy as orc
-
-    def barrier():
-        if dist:
-            tdist.barrier()
+    ctx = Ctx(dev, rank, world, dist)
 
     if args.train:
-        train_bench(args, dev, rank, world, barrier)
+        res = measure_train(ctx, args, args.model if args.model != "res15" else "res26-narrow", args.batch)
+        if rank == 0:
+            res.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+                        "scaling": "weak", "vs_baseline": None,
+                        "data": "synthetic N(0,1) [B,101,40] inputs + uniform labels resident in HBM"})
+            print(json.dumps(res), flush=True)
         if dist:
             tdist.destroy_process_group()
         return
 
+    from honk_amd import model as hm
+    from oracle import ref_numpy as orc
     cfg = dict(hm.find_config(args.model))
     torch.manual_seed(0)
     model = hm.find_model(args.model)(cfg).eval().to(dev)
     is_res = args.model.startswith("res")
     if not is_res and args.precision == "bf16":
         raise SystemExit("cnn models: --precision f32 or bf16x3")
-    model.honk_precision = args.precision
+    prec = args.precision
+    model.honk_precision = prec
     B = args.batch or (131072 if is_res else 65536)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(B, 101, 40, device=dev, generator=g)  # resident in HBM before timing
-    step_fn = model
+    log(f"world {world}: {args.model} {prec} x {B} clips/GPU, {args.steps} steps")
     if args.e2e:  # raw 1 s PCM windows instead of MFCC maps; MFCC runs on the GPU inside the step
         from honk_amd.audio import AudioPreprocessor
         ap = AudioPreprocessor()
         pcm = (torch.rand(B, 16000, device=dev, generator=g) * 2 - 1) * 0.3
-        x = pcm
 
         def step_fn(p):
             return model(ap.compute_mfccs_batch(p))
+        el, per, out, (kms, nlaunch, kflop) = ctx.timed(step_fn, pcm, args.steps, args.warmup)
+        idx = list(range(0, B, max(1, B // 32)))[:32]
+        xs = ap.compute_mfccs_batch(pcm[idx])
+        ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}, cfg,
+                          xs.cpu().numpy())
+        got = out[idx].cpu().numpy()
+        parity = {"top1_agreement_vs_oracle": float(np.mean(ref.argmax(1) == got.argmax(1))),
+                  "max_abs_logit_err_vs_oracle_f64": float(np.abs(ref - got).max()), "sample_clips": len(idx)}
+    else:
+        el, per, out, (kms, nlaunch, kflop) = ctx.timed(model, x, args.steps, args.warmup)
+        parity = _sample_parity(model, cfg, x, out, orc, B)
 
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            step_fn(x)
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        _native.timing_enable(True)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step_fn(x)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        barrier()
-        kms, nlaunch, kflop = _native.timing_read()
-        _native.timing_enable(False)
-    elapsed = hd.max_over_ranks(t1 - t0, device=dev)  # whole-job time = slowest rank
-
-    prec = args.precision
-    # cnn bf16x3: each algorithmic MAC is 3 bf16 MFMA products -> effective peak = bf16 peak / 3
-    peak = FP32_MFMA_PEAK_TFLOPS if prec == "f32" else BF16_MFMA_PEAK_TFLOPS / 3
-    # top-1 agreement / max logit error of the GPU logits vs the float64 oracle on a sample
-    idx = list(range(0, B, max(1, B // 32)))[:32]
-    xs = (ap.compute_mfccs_batch(x[idx]) if args.e2e else x[idx]).cpu().numpy()
-    ref = orc.forward({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()},
-                      cfg, xs)
-    got = out[idx].cpu().numpy()
-    top1 = float(np.mean(np.argmax(ref, 1) == np.argmax(got, 1)))
-    maxerr = float(np.abs(ref - got).max())
-
-    # the other precision modes of the same workload, reported beside the headline
     alts = {}
-    if is_res and not args.no_alt and not args.e2e:
-        for other in ("f32", "bf16"):
-            if other != prec:
-                alts[f"{other}_mode"] = measure_mode(other, model, x, args, dev, barrier, hd, _native, orc, cfg,
-                                                     B, world)
+    if not args.no_alt and not args.e2e:
+        if is_res:
+            for other in ("f32", "bf16"):
+                if other != prec:
+                    log(f"res {other} mode")
+                    alts[f"{other}_mode"] = measure_res(ctx, args, args.model, other, B, x=x, model=model)
+        del x
+        torch.cuda.empty_cache()
+        log("C2 cnn-trad-pool2")
+        alts["c2_cnn_trad_pool2"] = measure_c2(ctx, args)
+        torch.cuda.empty_cache()
+        log("C3 res8 bf16")
+        c3 = measure_res(ctx, args, "res8", "bf16", 131072)
+        c3["workload"] = "res8 eval forward in bf16 (config C3), 131,072 clips per GPU (1M over 8 GPUs)"
+        alts["c3_res8_bf16"] = c3
+        torch.cuda.empty_cache()
+        log("C5 res26-narrow training")
+        alts["c5_res26_narrow_train"] = measure_train(ctx, args)
 
-    c2 = None
-    if is_res and not args.no_alt and not args.e2e:
-        c2 = measure_c2(args, dev, barrier, hd, _native, orc, world, rank)
-
-    total = world * B * args.steps
-    value = total / elapsed
+    value = world * B * args.steps / el
     flop_clip = orc.flops_per_clip(cfg)
-    avg_ms = kms / max(nlaunch, 1)
-    achieved = (kflop / max(nlaunch, 1)) / (avg_ms * 1e-3) / 1e12 if nlaunch else None
+    if is_res:
+        roof = res_roofline(prec, cfg, kms, nlaunch, kflop, B, args.model)
+    else:
+        avg_ms = kms / max(nlaunch, 1)
+        ach = (kflop / max(nlaunch, 1)) / (avg_ms * 1e-3) / 1e12 if nlaunch else None
+        roof = {"bound": "mfma",
+                "kernel": ("honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM conv/linear, fp32 MFMA)"
+                           if prec == "f32" else
+                           "honk::cnn conv kernels in bf16x3 (3 bf16 MFMA products per MAC; peak = bf16 peak / 3)"),
+                "achieved": round(ach, 2) if ach else None, "peak": round(MODE_PEAK[prec], 1), "unit": "TFLOP/s",
+                "frac": round(ach / MODE_PEAK[prec], 4) if ach else None, "traffic": None,
+                "launches": nlaunch, "avg_launch_ms": round(avg_ms, 4), "flop_per_launch": kflop / max(nlaunch, 1)}
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        log("cpu baseline")
+        cpu = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -419,7 +571,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(el / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -430,31 +582,29 @@ def main():
                                    + WORKLOADS.get(args.model, f"{args.model} eval forward"),
                        "per_gpu_batch": B, "global_batch": world * B,
                        "parallelism": f"batch-shard x{world} (no data-path collective)"},
+            "per_rank_clips_s": [round(B * args.steps / t, 1) for t in per],
             "model_tflops": round(value * flop_clip / 1e12, 2),
-            "roofline": (res_roofline(prec, cfg, kms, nlaunch, kflop, B, args.model) if is_res else
-                         {"bound": "mfma",
-                          "kernel": ("honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM conv/linear, fp32 MFMA)"
-                                     if prec == "f32" else
-                                     "honk::cnn conv kernels in bf16x3 (conv1x3/conv2x3 for cnn-trad-pool2, "
-                                     "else conv_gemm_kernel<.., X3=true>; 3 bf16 MFMA products per MAC; "
-                                     "peak = bf16 peak / 3)"),
-                          "achieved": round(achieved, 2) if achieved else None,
-                          "peak": peak, "unit": "TFLOP/s",
-                          "frac": round(achieved / peak, 4) if achieved else None,
-                          "traffic": None,
-                          "launches": nlaunch, "avg_launch_ms": round(avg_ms, 4),
-                          "flop_per_launch": kflop / max(nlaunch, 1)}),
-            "parity": {"top1_agreement_vs_oracle": top1, "max_abs_logit_err_vs_oracle_f64": maxerr,
-                       "sample_clips": len(idx)},
+            "roofline": roof,
+            "parity": parity,
         }
         res.update(alts)
-        if c2 is not None:
-            res["c2_cnn_trad_pool2"] = c2
-        if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        if cpu is not None:
+            res["cpu_baseline"] = cpu
         print(json.dumps(res), flush=True)
     if dist:
+        tdist.barrier()
         tdist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, argv))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)")
+    rank_main(args)
 
 
 if __name__ == "__main__":

@@ -115,4 +115,10 @@ def batch_norm_train(x, bn):
     """nn.BatchNorm2d.forward in training mode (affine=False, momentum set): the
     module's num_batches_tracked bookkeeping, then the native normalisation."""
     bn.num_batches_tracked.add_(1)
-    return _BatchNormTrain.apply(x, bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps))
+    y = _BatchNormTrain.apply(x, bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps))
+    # the kernel updated the running stats through raw pointers: bump their version
+    # counters so caches keyed on (data_ptr, _version) -- SpeechResModel's packed eval
+    # weights -- see the change, as after PyTorch's own BatchNorm
+    torch.autograd.graph.increment_version(bn.running_mean)
+    torch.autograd.graph.increment_version(bn.running_var)
+    return y

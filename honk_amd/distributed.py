@@ -70,6 +70,34 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
+def gather_scalar(value: float, device=None) -> list:
+    """[value of rank 0, value of rank 1, ...] on every rank (one SUM all-reduce of a
+    one-hot vector; the bench's per-rank times)."""
+    rank, world = _ctx()
+    if world == 1:
+        return [float(value)]
+    if dist.get_backend() == "gloo":
+        device = None
+    t = torch.zeros(world, dtype=torch.float64, device=device)
+    t[rank] = value
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+def local_device_index(default: int = 0) -> int:
+    """The GPU this rank owns in a one-process-per-GPU job: LOCAL_RANK when set by the
+    launcher, else the global rank modulo the visible devices; `default` when
+    torch.distributed is not running with world > 1."""
+    import os
+    rank, world = _ctx()
+    if world == 1:
+        return default
+    if "LOCAL_RANK" in os.environ:
+        return int(os.environ["LOCAL_RANK"])
+    n = torch.cuda.device_count()
+    return rank % n if n else 0
+
+
 def world_info():
     return _ctx()
 

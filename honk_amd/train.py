@@ -74,8 +74,11 @@ def set_seed(config):
 
 
 def _select_device(config):
+    """utils/train.py:64,70,97: ``torch.cuda.set_device(config["gpu_no"])``.  In a
+    one-process-per-GPU job (torch.distributed up with world > 1) each rank takes
+    its own device (LOCAL_RANK) instead, so the replicas do not share one GPU."""
     if not config["no_cuda"]:
-        torch.cuda.set_device(config["gpu_no"])
+        torch.cuda.set_device(hd.local_device_index(config["gpu_no"]))
 
 
 def _whole_set_loader(dataset):
@@ -153,7 +156,7 @@ def train(config, datasets=None):
     hd.broadcast_module(model)
     flat = FlatParams(model)
     optimizer = _sgd(flat, config, config["lr"][0])
-    schedule_steps = list(config["schedule"])
+    schedule_steps = config["schedule"]  # the caller's list, extended in place (utils/train.py:100-101)
     schedule_steps.append(np.inf)
     sched_idx = 0
     criterion = nn.CrossEntropyLoss()

@@ -1,0 +1,88 @@
+"""bench.py's --gpus N launcher (CPU): the parent starts N rank processes with
+torchrun's environment, rank 0's single JSON line is the output, a failing rank
+ends the job with its status; the CPU-baseline thread count follows the
+process's CPU share."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import bench
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rank_envs_are_torchrun_like():
+    envs = bench.rank_envs(4, 29555, base={"PATH": "/bin"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29555"
+               and e["PATH"] == "/bin" for e in envs)
+
+
+def _run_spawn(tmp_path, body, n):
+    script = tmp_path / "rank.py"
+    script.write_text(textwrap.dedent(body))
+    drv = (f"import sys; sys.path.insert(0, {REPO!r}); import bench; "
+           f"sys.exit(bench.spawn_ranks({n}, ['--gpus', '{n}'], script={str(script)!r}))")
+    env = dict(os.environ, HONK_BENCH_ONE_GPU="1")
+    env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable, "-c", drv], env=env, capture_output=True, text=True, timeout=120)
+
+
+def test_spawn_two_ranks_one_json_line(tmp_path):
+    body = """
+        import json, os, sys
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        r, w = dist.get_rank(), dist.get_world_size()
+        assert int(os.environ["LOCAL_RANK"]) == r
+        sys.path.insert(0, os.environ.get("REPO_ROOT", "."))
+        import torch
+        t = torch.tensor([float(r + 1)])
+        dist.all_reduce(t)
+        print(f"rank {r} progress", file=sys.stderr)
+        if r == 0:
+            print(json.dumps({"n_gpus": w, "sum": float(t.item()), "argv": sys.argv[1:]}))
+        dist.barrier()
+        dist.destroy_process_group()
+    """
+    p = _run_spawn(tmp_path, body, 2)
+    assert p.returncode == 0, p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["sum"] == 3.0 and d["argv"] == ["--gpus", "2"]
+
+
+def test_spawn_failing_rank_ends_job(tmp_path):
+    body = """
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(3)
+        time.sleep(60)   # would wait for rank 1 forever in a real collective
+    """
+    p = _run_spawn(tmp_path, body, 2)
+    assert p.returncode == 3
+
+
+def test_cpu_share_bounded():
+    n = bench.cpu_share()
+    assert 1 <= n <= (os.cpu_count() or 1)
+    old = os.environ.get("OMP_NUM_THREADS")
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        assert bench.cpu_share() == 1
+    finally:
+        if old is None:
+            del os.environ["OMP_NUM_THREADS"]
+        else:
+            os.environ["OMP_NUM_THREADS"] = old
+
+
+def test_train_flops_res26_narrow():
+    from honk_amd import model as hm
+    cfg = dict(hm.find_config("res26-narrow"))
+    # 157.33 MFLOP forward, training ~3x forward - conv0 dgrad ~ 471 MFLOP
+    assert abs(bench.train_flops_per_clip(cfg) / 1e6 - 471) < 2
