@@ -64,6 +64,8 @@ def parse(argv=None):
                         "fp32 accumulation; 1e-4 parity), f32 (fp32 MFMA; 1e-4 parity) or bf16 (top-1 parity)")
     p.add_argument("--no-alt", action="store_true",
                    help="skip the extra measurements (other precision modes, C2, C3, C5)")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip C2/C3/C5 (keep the other res precision modes): the rocprof passes of tools/profile.sh")
     p.add_argument("--e2e", action="store_true",
                    help="serving pipeline: int16-scaled PCM [B,16000] in HBM -> GPU MFCC -> model -> logits")
     p.add_argument("--train", action="store_true",
@@ -532,6 +534,7 @@ def rank_main(args):
                 if other != prec:
                     log(f"res {other} mode")
                     alts[f"{other}_mode"] = measure_res(ctx, args, args.model, other, B, x=x, model=model)
+    if not args.no_alt and not args.e2e and not args.no_configs:
         del x
         torch.cuda.empty_cache()
         log("C2 cnn-trad-pool2")

@@ -1,0 +1,83 @@
+"""Replays the reference-generated training fixtures (tests/golden/train_*.npz,
+written by make_train_golden.py from /root/reference/utils/train.py's own step)
+on honk_amd's model + FlatSGD, on CPU or on the GPU's native training path."""
+import os
+
+import numpy as np
+import torch
+
+from honk_amd import model as hm
+from honk_amd.optim import FlatParams, FlatSGD
+from oracle import ref_numpy as orc
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TRAIN_CASES = ("train_res8-narrow", "train_res26-narrow", "train_res15-narrow")
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def build(z, device):
+    """honk_amd model at the fixture's starting point (weights from the PCG64 seed,
+    BN running stats as stored)."""
+    name = str(z["model"])
+    cfg = dict(hm.find_config(name))
+    params = orc.make_params(cfg, int(z["seed"]))
+    for k in params:
+        if f"init__{k}" in z.files:
+            params[k] = z[f"init__{k}"]
+    np.testing.assert_array_equal(orc.params_checksum(params), z["checksum"])
+    m = hm.find_model(name)(cfg)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v, dtype=np.float32 if np.asarray(v).dtype != np.int64
+                                                       else np.int64)) for k, v in params.items()})
+    return cfg, m.to(device)
+
+
+def replay(name, device):
+    """Run the fixture's steps; returns dict(loss=[...], g=[{k: grad}], p=[{k: param}], b=[{k: buffer}])."""
+    z = load(name)
+    cfg, m = build(z, device)
+    flat = FlatParams(m)
+    opt = FlatSGD(flat, lr=float(z["lr"]), momentum=float(z["momentum"]), weight_decay=float(z["weight_decay"]),
+                  nesterov=bool(z["nesterov"]))
+    x = torch.from_numpy(z["x"]).to(device)
+    y = torch.from_numpy(z["y"]).to(device)
+    crit = torch.nn.CrossEntropyLoss()
+    out = dict(loss=[], g=[], p=[], b=[])
+    for _ in range(int(z["steps"])):
+        m.train()
+        opt.zero_grad()
+        loss = crit(m(x), y)
+        loss.backward()
+        out["g"].append({k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()})
+        opt.step()
+        out["loss"].append(float(loss.item()))
+        out["p"].append({k: p.detach().cpu().numpy().copy() for k, p in m.named_parameters()})
+        out["b"].append({k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items() if "running_" in k})
+    return z, out
+
+
+def rel_err(got, ref):
+    """max |got - ref| / max |ref| (0 when both are 0)."""
+    scale = float(np.abs(ref).max())
+    d = float(np.abs(got.astype(np.float64) - ref.astype(np.float64)).max())
+    return d / scale if scale > 0 else d
+
+
+def compare(z, out, grad_rtol, param_atol, loss_atol, buf_rtol):
+    """Every step's loss, gradients, updated parameters and running stats vs the fixture.
+    Returns the worst (grad rel err, param abs err, loss abs err, buffer rel err)."""
+    worst = [0.0, 0.0, 0.0, 0.0]
+    for s in range(int(z["steps"])):
+        worst[2] = max(worst[2], abs(out["loss"][s] - float(z["loss"][s])))
+        for k in out["g"][s]:
+            worst[0] = max(worst[0], rel_err(out["g"][s][k], z[f"g{s}__{k}"]))
+            worst[1] = max(worst[1], float(np.abs(out["p"][s][k] - z[f"p{s}__{k}"]).max()))
+        for k in out["b"][s]:
+            worst[3] = max(worst[3], rel_err(out["b"][s][k], z[f"b{s}__{k}"]))
+    assert worst[2] <= loss_atol, ("loss", worst)
+    assert worst[0] <= grad_rtol, ("grad", worst)
+    assert worst[1] <= param_atol, ("param", worst)
+    assert worst[3] <= buf_rtol, ("running stats", worst)
+    return worst

@@ -11,7 +11,7 @@ STEPS=${STEPS:-2}
 export TMPDIR=/tmp
 OUT=$PWD/gpurun_out/prof
 mkdir -p "$OUT"
-ARGS="bench.py --batch $BATCH --steps $STEPS --warmup 1 --no-cpu-baseline"
+ARGS="bench.py --batch $BATCH --steps $STEPS --warmup 1 --no-cpu-baseline ${PROF_EXTRA:---no-configs}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o ${TAG}_trace --output-format csv -- python3 $ARGS > "$OUT/${TAG}_trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT" -o ${TAG}_fetch --output-format csv -- python3 $ARGS > "$OUT/${TAG}_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT" -o ${TAG}_write --output-format csv -- python3 $ARGS > "$OUT/${TAG}_write.log" 2>&1
