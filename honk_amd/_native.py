@@ -53,10 +53,10 @@ _PROTOS = {
                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "honk_sgd_step_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64, ctypes.c_float, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p]),
-    "honk_conv3x3_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 4
+    "honk_conv3x3_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 5
                          + [ctypes.c_void_p]),
-    "honk_conv3x3_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64] + [ctypes.c_int32] * 3),
-    "honk_conv3x3_wgrad_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 3
+    "honk_conv3x3_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64] + [ctypes.c_int32] * 4),
+    "honk_conv3x3_wgrad_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 4
                                + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "honk_bn_train_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int64]),
     "honk_bn_train_fwd_f32": (ctypes.c_int, [c_f32p] * 6 + [ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,

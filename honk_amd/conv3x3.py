@@ -1,9 +1,10 @@
 """Training-mode res block convolutions on the gfx950 kernels (libhonk_hip.so).
 
-``conv3x3(x, w)`` is the ``nn.Conv2d(C, C, 3, padding=1, bias=False)`` of
-SpeechResModel's block stack (/root/reference/utils/model.py:94-98, use_dilation
-False: res8/res26 and -narrow) as an autograd function whose forward, input
-gradient and weight gradient are ``honk_conv3x3_f32`` / ``honk_conv3x3_wgrad_f32``;
+``conv3x3(x, w, d)`` is the ``nn.Conv2d(C, C, 3, padding=d, dilation=d, bias=False)``
+of SpeechResModel's block stack (/root/reference/utils/model.py:94-98: d = 1 for
+res8/res26 and -narrow, d = 2**(i//3) for res15 and res15-narrow) as an autograd
+function whose forward, input gradient and weight gradient are
+``honk_conv3x3_f32`` / ``honk_conv3x3_wgrad_f32``;
 ``batch_norm_train(x, bn)`` is the blocks' train-mode ``BatchNorm2d(affine=False)``
 (model.py:100, 117-118) on ``honk_bn_train_fwd/bwd_f32``.  The rest of the
 training graph (ReLU, residual, conv0, pooling, mean, Linear, loss) stays PyTorch
@@ -20,29 +21,32 @@ CHANNELS = (19, 45)
 
 
 def supported(x, conv) -> bool:
-    """The native kernels cover dilation-1, padding-1, bias-free 3x3 convs with C in CHANNELS."""
+    """The native kernels cover bias-free 3x3 convs with padding == dilation (the res
+    blocks' "same" convs) and C in CHANNELS."""
+    d = tuple(conv.dilation)
     return (x.is_cuda and x.dtype == torch.float32 and conv.weight.shape[0] in CHANNELS
-            and tuple(conv.dilation) == (1, 1) and tuple(conv.padding) == (1, 1) and conv.bias is None)
+            and tuple(conv.kernel_size) == (3, 3) and d[0] == d[1] and 1 <= d[0] <= 64
+            and tuple(conv.padding) == d and tuple(conv.stride) == (1, 1) and conv.bias is None)
 
 
-def _conv(x, w, flip):
+def _conv(x, w, flip, d=1):
     x = x.contiguous()
     B, C, H, W = x.shape
     y = torch.empty_like(x)
-    _native.check(_native.load().honk_conv3x3_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W,
+    _native.check(_native.load().honk_conv3x3_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W, d,
                                                   1 if flip else 0, _native.stream_handle(x.device)),
                   "honk_conv3x3_f32")
     return y
 
 
-def _wgrad(x, dy):
+def _wgrad(x, dy, d=1):
     x, dy = x.contiguous(), dy.contiguous()
     B, C, H, W = x.shape
     lib = _native.load()
     dw = torch.empty(C, C, 3, 3, dtype=torch.float32, device=x.device)
-    nbytes = lib.honk_conv3x3_wgrad_workspace_bytes(B, C, H, W)
+    nbytes = lib.honk_conv3x3_wgrad_workspace_bytes(B, C, H, W, d)
     ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=x.device)
-    _native.check(lib.honk_conv3x3_wgrad_f32(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), B, C, H, W,
+    _native.check(lib.honk_conv3x3_wgrad_f32(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), B, C, H, W, d,
                                              ws.data_ptr(), nbytes, _native.stream_handle(x.device)),
                   "honk_conv3x3_wgrad_f32")
     return dw
@@ -50,22 +54,23 @@ def _wgrad(x, dy):
 
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, d):
         w = w.contiguous()
         ctx.save_for_backward(x, w)
-        return _conv(x, w, flip=False)
+        ctx.dil = d
+        return _conv(x, w, flip=False, d=d)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dy = dy.contiguous()
-        dx = _conv(dy, w, flip=True) if ctx.needs_input_grad[0] else None
-        dw = _wgrad(x, dy) if ctx.needs_input_grad[1] else None
-        return dx, dw
+        dx = _conv(dy, w, flip=True, d=ctx.dil) if ctx.needs_input_grad[0] else None
+        dw = _wgrad(x, dy, d=ctx.dil) if ctx.needs_input_grad[1] else None
+        return dx, dw, None
 
 
-def conv3x3(x, w):
-    return _Conv3x3.apply(x, w)
+def conv3x3(x, w, d=1):
+    return _Conv3x3.apply(x, w, int(d))
 
 
 # -- train-mode BatchNorm2d(affine=False) (model.py:100, 117-118 in training) -------

@@ -52,10 +52,10 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
 }
 
 // ---------------------------------------------------------------------------- //
-// Training-mode 3x3 convolutions of the res block stack (dilation 1, padding 1,
-// no bias; model.py:94-98 with use_dilation False), fp32 NCHW like the PyTorch
-// tensors around them (train-mode BatchNorm, ReLU, residual and the loss stay
-// PyTorch ops on the device):
+// Training-mode 3x3 convolutions of the res block stack (dilation d, padding d,
+// no bias; model.py:94-98: d = 1 for res8/res26, 2**(i//3) for res15), fp32 NCHW
+// like the PyTorch tensors around them (train-mode BatchNorm, ReLU, residual and
+// the loss stay PyTorch ops on the device):
 //   conv3x3_kernel<C,NP>: y = conv(x, w) (flip 0) or the input gradient
 //     dx = conv(dy, w'), w'[o][i][t] = w[i][o][8-t] (flip 1) -- the transform is
 //     applied while the weights are staged into LDS as [in][tap][out].
@@ -63,9 +63,14 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
 //     the partials in a fixed order (deterministic, no atomics).
 // VALU direct convolution: 19 (45) channels are far from an MFMA tile (19 -> 32
 // is 2.8x the work), and gfx950's fp32 VALU FMA rate equals its fp32 MFMA rate.
-// A tile is a band of TH rows of one clip: its (TH+2) x (W+2) zero-padded input
-// rows of every channel are staged in LDS once; each thread owns NP output
-// pixels x all C outputs (weights read as LDS broadcasts, 4 per ds_read_b128).
+// A dilated 3x3 conv couples row h only with rows h -/+ d, so the rows of one
+// residue class r = h mod d are an independent problem (the inference row-band
+// kernel's decomposition).  A tile is a band of TH class rows (rows r + (k TH + j) d)
+// of one clip at full width: its (TH+2) x (W+2d) zero-padded input rows of every
+// channel are staged in LDS once (one halo class row above/below, d zero columns
+// left/right); tap (ky, kx) of staged pixel (j, w) is (j + ky, w + kx d).  Each
+// thread owns NP output pixels x all C outputs (weights read as LDS broadcasts,
+// 4 per ds_read_b128).  d = 1 is the plain band of TH rows.
 // ---------------------------------------------------------------------------- //
 constexpr int TC_XL = 64 * 1024;  // bytes of the staged input tile (wgrad: and of its dy tile)
 #ifndef HONK_TC_XLC
@@ -79,11 +84,45 @@ struct TC {
   static constexpr int WL = C * 9 * CW;    // floats of the staged weights
 };
 
+// class-band geometry of one clip (dilation d, TH class rows per band): classes
+// r < rem hold H/d + 1 rows (nb1 bands), the others H/d rows (nb0 bands)
+struct ClassBands {
+  int d, TH, rem, nb1, nb0, nband;  // nband = bands per clip
+};
+static inline ClassBands class_bands(int H, int d, int TH) {
+  ClassBands g;
+  const int q = H / d;
+  g.d = d;
+  g.TH = TH;
+  g.rem = H - q * d;
+  g.nb1 = (q + 1 + TH - 1) / TH;
+  g.nb0 = (q + TH - 1) / TH;
+  g.nband = g.rem * g.nb1 + (d - g.rem) * g.nb0;
+  return g;
+}
+// band bi of a clip -> residue class r, first class row k0, rows in the band
+__device__ __forceinline__ void band_of(const ClassBands& g, int H, int bi, int& r, int& k0, int& th) {
+  int k;
+  if (bi < g.rem * g.nb1) {
+    r = bi / g.nb1;
+    k = bi - r * g.nb1;
+  } else {
+    const int bj = bi - g.rem * g.nb1;
+    const int rr = bj / g.nb0;
+    k = bj - rr * g.nb0;
+    r = g.rem + rr;
+  }
+  const int rows = (H - r + g.d - 1) / g.d;  // class rows of class r
+  k0 = k * g.TH;
+  th = min(g.TH, rows - k0);
+}
+
 struct Conv3Args {
   const float* x;  // [B][C][H][W]
   const float* w;  // OIHW [C][C][3][3]
   float* y;        // [B][C][H][W]
-  int B, H, W, TH, nband, flip;
+  int B, H, W, flip;
+  ClassBands g;
 };
 
 typedef float tf2 __attribute__((ext_vector_type(2)));
@@ -100,15 +139,17 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
     if (o < C) v = a.flip ? a.w[(in * C + o) * 9 + 8 - t] : a.w[(o * C + in) * 9 + t];
     wl[i] = v;
   }
-  const int Wp = a.W + 2;
-  for (int tile = blockIdx.x; tile < a.B * a.nband; tile += gridDim.x) {
-    const int b = tile / a.nband, h0 = (tile - b * a.nband) * a.TH;
-    const int th = min(a.TH, a.H - h0), rows = th + 2, plane = rows * Wp;
+  const int d = a.g.d, Wp = a.W + 2 * d;
+  for (int tile = blockIdx.x; tile < a.B * a.g.nband; tile += gridDim.x) {
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, a.H, tile - b * a.g.nband, r, k0, th);
+    const int rows = th + 2, plane = rows * Wp;
     __syncthreads();  // previous tile's readers done (and the weights staged)
     const float* xb = a.x + (size_t)b * C * a.H * a.W;
     for (int i = tid; i < C * plane; i += 256) {
-      const int c = i / plane, rc = i - c * plane, r = rc / Wp, col = rc - r * Wp;
-      const int h = h0 - 1 + r, w = col - 1;
+      const int c = i / plane, rc = i - c * plane, rr = rc / Wp, col = rc - rr * Wp;
+      const int h = r + (k0 - 1 + rr) * d, w = col - d;
       xl[i] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
     }
     __syncthreads();
@@ -118,8 +159,8 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int q = tid + k * 256;
-      const int r = q / a.W, col = q - r * a.W;
-      base[k] = q < th * a.W ? r * Wp + col : 0;
+      const int j = q / a.W, col = q - j * a.W;
+      base[k] = q < th * a.W ? j * Wp + col : 0;
 #pragma unroll
       for (int o = 0; o < CW / 2; ++o) acc[k][o] = tf2{0.f, 0.f};
     }
@@ -128,7 +169,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
       const float4* wc = (const float4*)(wl + ci * 9 * CW);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int toff = (t / 3) * Wp + (t % 3);
+        const int toff = (t / 3) * Wp + (t % 3) * d;
         tf2 xv[NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
@@ -147,13 +188,15 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
         }
       }
     }
-    float* yb = a.y + (size_t)b * C * a.H * a.W + (size_t)h0 * a.W;
+    float* yb = a.y + (size_t)b * C * a.H * a.W;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int q = tid + k * 256;
       if (q < th * a.W) {
+        const int j = q / a.W, col = q - j * a.W;
+        const size_t pix = (size_t)(r + (k0 + j) * d) * a.W + col;
 #pragma unroll
-        for (int o = 0; o < C; ++o) yb[(size_t)o * a.H * a.W + q] = acc[k][o >> 1][o & 1];
+        for (int o = 0; o < C; ++o) yb[(size_t)o * a.H * a.W + pix] = acc[k][o >> 1][o & 1];
       }
     }
   }
@@ -163,7 +206,8 @@ struct WgradArgs {
   const float* x;   // [B][C][H][W]
   const float* dy;  // [B][C][H][W]
   float* part;      // [gridDim.x][C][C][9] partial sums
-  int B, H, W, TH, nband;
+  int B, H, W;
+  ClassBands g;
 };
 
 // wgrad: 512 threads = NG groups of TG threads (+ idle); group g takes the tile's
@@ -187,7 +231,7 @@ __global__ __launch_bounds__(512) void wgrad3x3_kernel(WgradArgs a) {
   const int tid = threadIdx.x;
   const int grp = tid / TG, u = tid - grp * TG;
   const bool active = grp < NG;
-  const int Wp = a.W + 2;
+  const int d = a.g.d, Wp = a.W + 2 * d;
   tf2 acc[PJ][CW / 2];
   int jo[PJ];  // per owned column: LDS offset of (ci, tap) in the tile (row 0, col 0), -1 if none
 #pragma unroll
@@ -195,20 +239,23 @@ __global__ __launch_bounds__(512) void wgrad3x3_kernel(WgradArgs a) {
 #pragma unroll
     for (int o = 0; o < CW / 2; ++o) acc[n][o] = tf2{0.f, 0.f};
   }
-  for (int tile = blockIdx.x; tile < a.B * a.nband; tile += gridDim.x) {
-    const int b = tile / a.nband, h0 = (tile - b * a.nband) * a.TH;
-    const int th = min(a.TH, a.H - h0), rows = th + 2, plane = rows * Wp, npx = th * a.W;
+  for (int tile = blockIdx.x; tile < a.B * a.g.nband; tile += gridDim.x) {
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, a.H, tile - b * a.g.nband, r, k0, th);
+    const int rows = th + 2, plane = rows * Wp, npx = th * a.W;
     __syncthreads();
     const float* xb = a.x + (size_t)b * C * a.H * a.W;
     for (int i = tid; i < C * plane; i += 512) {
-      const int c = i / plane, rc = i - c * plane, r = rc / Wp, col = rc - r * Wp;
-      const int h = h0 - 1 + r, w = col - 1;
+      const int c = i / plane, rc = i - c * plane, rr = rc / Wp, col = rc - rr * Wp;
+      const int h = r + (k0 - 1 + rr) * d, w = col - d;
       xl[i] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
     }
-    const float* db = a.dy + (size_t)b * C * a.H * a.W + (size_t)h0 * a.W;
+    const float* db = a.dy + (size_t)b * C * a.H * a.W;
     for (int i = tid; i < CW * npx; i += 512) {  // dy transposed to [pixel][out]
       const int o = i / npx, p = i - o * npx;
-      dl[p * CW + o] = o < C ? db[(size_t)o * a.H * a.W + p] : 0.f;
+      const int j = p / a.W, col = p - j * a.W;
+      dl[p * CW + o] = o < C ? db[(size_t)o * a.H * a.W + (size_t)(r + (k0 + j) * d) * a.W + col] : 0.f;
     }
     __syncthreads();
     if (active) {
@@ -216,11 +263,11 @@ __global__ __launch_bounds__(512) void wgrad3x3_kernel(WgradArgs a) {
       for (int n = 0; n < PJ; ++n) {
         const int j = PJ * u + n;
         const int ci = j / 9, t = j - ci * 9;
-        jo[n] = j < C * 9 ? ci * plane + (t / 3) * Wp + (t % 3) : 0;
+        jo[n] = j < C * 9 ? ci * plane + (t / 3) * Wp + (t % 3) * d : 0;
       }
       for (int p = grp; p < npx; p += NG) {
-        const int r = p / a.W, col = p - r * a.W;
-        const int po = r * Wp + col;
+        const int j = p / a.W, col = p - j * a.W;
+        const int po = j * Wp + col;
         tf2 xv[PJ];
 #pragma unroll
         for (int n = 0; n < PJ; ++n) {
@@ -409,20 +456,22 @@ static int bn_slices(int B, int C) {
   return S < 1 ? 1 : S;
 }
 
-// rows per tile: the staged input (C planes of (TH+2) x (W+2)) and (wgrad) its dy
-// within TC_XL, at most 1024 pixels (4 per thread); bands balanced over the clip
-static int tc_rows(int C, int H, int W, bool conv = false) {
-  int th = (conv && C <= 20 ? TC_XLC : TC_XL) / 4 / (C * (W + 2)) - 2;
+// class rows per tile: the staged input (C planes of (TH+2) x (W+2d)) and (wgrad)
+// its dy within TC_XL, at most 1024 pixels (4 per thread); bands balanced over the
+// (longest) class
+static int tc_rows(int C, int H, int W, int d, bool conv = false) {
+  int th = (conv && C <= 20 ? TC_XLC : TC_XL) / 4 / (C * (W + 2 * d)) - 2;
   const int byp = (C <= 20 ? 1024 : 512) / W;  // conv3x3_kernel: NP <= 4 (19 maps) / 2 (45 maps)
   if (th > byp) th = byp;
   if (!conv) {
     const int byd = TC_XL / 4 / (((C + 3) & ~3) * W);
     if (th > byd) th = byd;
   }
-  if (th > H) th = H;
+  const int hc = (H + d - 1) / d;  // rows of the longest class
+  if (th > hc) th = hc;
   if (th < 1) return 0;
-  const int nb = (H + th - 1) / th;
-  return (H + nb - 1) / nb;
+  const int nb = (hc + th - 1) / th;
+  return (hc + nb - 1) / nb;
 }
 static int tc_grid(int64_t tiles) {
   const int64_t g = 2 * (int64_t)cu_count();
@@ -448,30 +497,32 @@ extern "C" int honk_sgd_step_f32(float* params, const float* grads, float* momen
 }
 
 namespace {
-int tc_check(const void* a, const void* b, const void* c, int64_t batch, int32_t ch, int32_t h, int32_t w) {
+int tc_check(const void* a, const void* b, const void* c, int64_t batch, int32_t ch, int32_t h, int32_t w,
+             int32_t d) {
   if (!a || !b || !c) return fail(HONK_ERR_ARG, "null pointer argument");
   if (batch < 0 || h < 1 || w < 1) return fail(HONK_ERR_ARG, "bad conv3x3 shape (B=%lld H=%d W=%d)", (long long)batch, h, w);
+  if (d < 1 || d > 64) return fail(HONK_ERR_ARG, "conv3x3: dilation %d (1..64)", d);
   if (ch != 19 && ch != 45) return fail(HONK_ERR_UNSUPPORTED, "conv3x3 training kernels: C=%d (19 or 45)", ch);
-  if (train::tc_rows(ch, h, w) < 1 || train::tc_rows(ch, h, w, true) < 1) return fail(HONK_ERR_UNSUPPORTED, "conv3x3: width %d too large", w);
+  if (train::tc_rows(ch, h, w, d) < 1 || train::tc_rows(ch, h, w, d, true) < 1)
+    return fail(HONK_ERR_UNSUPPORTED, "conv3x3: width %d at dilation %d too large", w, d);
   if (batch * (int64_t)h > 0x3fffffff) return fail(HONK_ERR_ARG, "conv3x3: batch too large");
   return HONK_OK;
 }
 }  // namespace
 
 extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
-                                int32_t w_, int32_t flip, void* stream) {
-  int rc = tc_check(x, w, y, batch, c, h, w_);
+                                int32_t w_, int32_t dil, int32_t flip, void* stream) {
+  int rc = tc_check(x, w, y, batch, c, h, w_, dil);
   if (rc) return rc;
   if (batch == 0) return HONK_OK;
   train::Conv3Args a;
   a.x = x; a.w = w; a.y = y;
   a.B = (int)batch; a.H = h; a.W = w_; a.flip = flip ? 1 : 0;
-  a.TH = train::tc_rows(c, h, w_, true);
-  a.nband = (h + a.TH - 1) / a.TH;
-  const int grid = train::tc_grid((int64_t)a.B * a.nband);
+  a.g = train::class_bands(h, dil, train::tc_rows(c, h, w_, dil, true));
+  const int grid = train::tc_grid((int64_t)a.B * a.g.nband);
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  const int np = (int)cdiv((int64_t)a.TH * w_, 256);  // output pixels per thread
+  const int np = (int)cdiv((int64_t)a.g.TH * w_, 256);  // output pixels per thread
   if (c == 19) {
     if (np <= 1) hipLaunchKernelGGL((train::conv3x3_kernel<19, 1>), dim3(grid), dim3(256), 0, st, a);
     else if (np == 2) hipLaunchKernelGGL((train::conv3x3_kernel<19, 2>), dim3(grid), dim3(256), 0, st, a);
@@ -486,17 +537,18 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   return HONK_OK;
 }
 
-extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_) {
-  if (batch < 1 || (c != 19 && c != 45) || h < 1 || w_ < 1) return 0;
-  const int th = train::tc_rows(c, h, w_);
+extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil) {
+  if (batch < 1 || (c != 19 && c != 45) || h < 1 || w_ < 1 || dil < 1 || dil > 64) return 0;
+  const int th = train::tc_rows(c, h, w_, dil);
   if (th < 1) return 0;
-  const int64_t tiles = batch * ((h + th - 1) / th);
+  const int64_t tiles = batch * train::class_bands(h, dil, th).nband;
   return (size_t)train::tc_grid(tiles) * c * c * 9 * sizeof(float);
 }
 
 extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
-                                      int32_t h, int32_t w_, void* workspace, size_t ws_bytes, void* stream) {
-  int rc = tc_check(x, dy, dw, batch, c, h, w_);
+                                      int32_t h, int32_t w_, int32_t dil, void* workspace, size_t ws_bytes,
+                                      void* stream) {
+  int rc = tc_check(x, dy, dw, batch, c, h, w_, dil);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   const int n = c * c * 9;
@@ -504,14 +556,13 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
     HONK_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)n * sizeof(float), st));
     return HONK_OK;
   }
-  const size_t need = honk_conv3x3_wgrad_workspace_bytes(batch, c, h, w_);
+  const size_t need = honk_conv3x3_wgrad_workspace_bytes(batch, c, h, w_, dil);
   if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
   train::WgradArgs a;
   a.x = x; a.dy = dy; a.part = (float*)workspace;
   a.B = (int)batch; a.H = h; a.W = w_;
-  a.TH = train::tc_rows(c, h, w_);
-  a.nband = (h + a.TH - 1) / a.TH;
-  const int grid = train::tc_grid((int64_t)a.B * a.nband);
+  a.g = train::class_bands(h, dil, train::tc_rows(c, h, w_, dil));
+  const int grid = train::tc_grid((int64_t)a.B * a.g.nband);
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
   if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((train::wgrad3x3_kernel<45>), dim3(grid), dim3(512), 0, st, a);

@@ -17,8 +17,9 @@ Forward dispatch:
   extension is missing this raises; there is no silent fallback.
 * CPU tensors, or training mode (autograd) -> the same PyTorch module ops the
   reference runs (the reference is pure PyTorch; this keeps ``--no_cuda``
-  evaluation and ``train()`` working).  Native training kernels are future work
-  (DESIGN.md).
+  evaluation and ``train()`` working); on ROCm tensors in training mode the
+  block convs (every dilation) and their train-mode BatchNorms run on the native
+  training kernels (``honk_amd/conv3x3.py``).
 """
 from __future__ import annotations
 
@@ -154,7 +155,7 @@ class SpeechResModel(SerializableModule):
     # -- reference forward (CPU tensors / training mode): model.py:104-121 --
     # native_convs: training on a ROCm tensor runs the block convs (conv1..convN)
     # on honk_conv3x3_f32 / honk_conv3x3_wgrad_f32 where they cover the shape
-    # (dilation 1, 19 or 45 maps) and the train-mode BatchNorms on honk_bn_train_*
+    # (any dilation, 19 or 45 maps) and the train-mode BatchNorms on honk_bn_train_*
     # (honk_amd/conv3x3.py); ReLU, residual, conv0, pool, mean, Linear and the loss
     # stay PyTorch autograd
     def _torch_forward(self, x, native_convs=False):
@@ -162,7 +163,7 @@ class SpeechResModel(SerializableModule):
         for i in range(self.n_layers + 1):
             conv = getattr(self, "conv{}".format(i))
             if native_convs and i > 0 and _conv3x3.supported(x, conv):
-                y = F.relu(_conv3x3.conv3x3(x, conv.weight))
+                y = F.relu(_conv3x3.conv3x3(x, conv.weight, conv.dilation[0]))
             else:
                 y = F.relu(conv(x))
             if i == 0:

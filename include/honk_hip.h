@@ -132,20 +132,21 @@ int honk_sgd_step_f32(float* params, const float* grads, float* momentum_buf, in
                       float momentum, float weight_decay, float grad_scale, int32_t nesterov, void* stream);
 
 /*
- * Training-mode 3x3 convolutions of the res block stack (padding 1, dilation 1, no
- * bias: model.py:94-98 with use_dilation False -- res8/res26 and -narrow), replacing
- * the nn.Conv2d forward/backward that utils/train.py:131-134 runs through autograd.
- * NCHW fp32, channels C in {19, 45}; w is the OIHW [C][C][3][3] conv weight.
+ * Training-mode 3x3 convolutions of the res block stack (dilation d, padding d, no
+ * bias: model.py:94-98 -- d = 1 for res8/res26 and -narrow, d = 2**(i//3) for
+ * res15 and res15-narrow), replacing the nn.Conv2d forward/backward that
+ * utils/train.py:131-134 runs through autograd.  NCHW fp32, channels C in {19, 45};
+ * w is the OIHW [C][C][3][3] conv weight; 1 <= dil <= 64.
  *   flip = 0: y = conv(x, w)                                (forward)
  *   flip = 1: y = conv(x, w'), w'[o][i][t] = w[i][o][8-t]   (input gradient: x = dy)
  */
 int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h, int32_t w_,
-                     int32_t flip, void* stream);
-/* dw[o][i][ky][kx] = sum_{b,h,w} dy[b][o][h][w] * x[b][i][h+ky-1][w+kx-1] (zero padded);
+                     int32_t dil, int32_t flip, void* stream);
+/* dw[o][i][ky][kx] = sum_{b,h,w} dy[b][o][h][w] * x[b][i][h+(ky-1)d][w+(kx-1)d] (zero padded);
  * deterministic: per-workgroup partials in the workspace, summed in a fixed order. */
-size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_);
+size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil);
 int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c, int32_t h,
-                           int32_t w_, void* workspace, size_t workspace_bytes, void* stream);
+                           int32_t w_, int32_t dil, void* workspace, size_t workspace_bytes, void* stream);
 /*
  * Train-mode BatchNorm2d(affine=False) (model.py:100 in training, nn.BatchNorm2d
  * semantics): y = (x - mean) * invstd with the biased batch variance over (B, H, W);

@@ -27,19 +27,24 @@ def _rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("C,B,H,W", [(19, 3, 50, 20), (45, 2, 25, 13), (19, 1, 7, 5), (45, 3, 50, 20), (19, 5, 101, 40)])
-def test_conv3x3_kernels_match_torch(C, B, H, W):
-    g = torch.Generator(device=DEV).manual_seed(C * 100 + H)
+@pytest.mark.parametrize("C,B,H,W,d", [(19, 3, 50, 20, 1), (45, 2, 25, 13, 1), (19, 1, 7, 5, 1), (45, 3, 50, 20, 1),
+                                       (19, 5, 101, 40, 1), (45, 2, 101, 40, 2), (19, 3, 101, 40, 4),
+                                       (45, 2, 101, 40, 8), (45, 2, 101, 40, 16), (19, 2, 101, 40, 16),
+                                       (19, 2, 9, 5, 3)])
+def test_conv3x3_kernels_match_float64(C, B, H, W, d):
+    """forward / input grad / weight grad vs float64 (CPU) at every res dilation:
+    within 1e-5 of each result's max |value| (fp32 accumulation over 9C or B*H*W terms)."""
+    g = torch.Generator(device=DEV).manual_seed(C * 100 + H + d)
     x = torch.randn(B, C, H, W, device=DEV, generator=g)
     w = torch.randn(C, C, 3, 3, device=DEV, generator=g) * 0.1
     dy = torch.randn(B, C, H, W, device=DEV, generator=g)
-    y = hc._conv(x, w, flip=False)
-    torch.testing.assert_close(y, F.conv2d(x, w, padding=1), rtol=1e-5, atol=1e-5)
-    dx = hc._conv(dy, w, flip=True)
-    ref_dx = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=1)
-    torch.testing.assert_close(dx, ref_dx, rtol=1e-5, atol=1e-5)
-    dw = hc._wgrad(x, dy)
-    ref_dw = torch.nn.grad.conv2d_weight(x, w.shape, dy, padding=1)
+    x64, w64, dy64 = x.double().cpu(), w.double().cpu(), dy.double().cpu()
+    y = hc._conv(x, w, flip=False, d=d)
+    assert _rel(y, F.conv2d(x64, w64, padding=d, dilation=d)) < 1e-5
+    dx = hc._conv(dy, w, flip=True, d=d)
+    assert _rel(dx, torch.nn.grad.conv2d_input(x64.shape, w64, dy64, padding=d, dilation=d)) < 1e-5
+    dw = hc._wgrad(x, dy, d=d)
+    ref_dw = torch.nn.grad.conv2d_weight(x64, w64.shape, dy64, padding=d, dilation=d)
     assert _rel(dw, ref_dw) < 1e-5, _rel(dw, ref_dw)
 
 

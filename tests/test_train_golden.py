@@ -7,11 +7,14 @@ torch.optim.SGD with momentum / weight decay / nesterov as in
 * CPU, 2 ranks over gloo: the data-parallel step (broadcast, ONE all-reduce of the
   flat bucket, SGD on the mean) reproduces the reference's 2-shard mean-gradient
   step (train_dp2_*.npz, DDP semantics of config C5).
-* GPU: the native training path (gfx950 block-conv fwd / dgrad / wgrad and
-  train-BN kernels, fused SGD) within stated fp32 tolerances: every gradient
-  within 2e-3 of its tensor's max |grad| (train-mode BN divides by the batch
-  std of a 3-6 clip batch, which amplifies fp32 reassociation), updated weights
-  within 1e-5 absolute, loss within 1e-5, running stats within 1e-4 relative.
+* GPU: the native training path (gfx950 block-conv fwd / dgrad / wgrad at every
+  dilation, train-BN kernels, fused SGD) is at least as accurate as the
+  reference's own fp32 step: per step, its gradients (max |err| / max |grad| per
+  tensor), updated weights, loss and running stats are no farther from the
+  float64 step than 2x the reference fp32's distance (floors 1e-4 / 1e-6 / 1e-5 /
+  1e-5).  A plain fp32 tolerance does not work here: on res26-narrow the
+  reference's own fp32 gradients are 1.5e-2 from float64 (train-mode BatchNorm of
+  a 4-clip batch divides by near-zero batch variances of almost-dead channels).
 """
 import os
 import socket
@@ -26,7 +29,6 @@ import train_golden_util as tg
 from honk_amd import distributed as hd
 from honk_amd.optim import FlatParams, FlatSGD
 
-GPU_TOL = dict(grad_rtol=2e-3, param_atol=1e-5, loss_atol=1e-5, buf_rtol=1e-4)
 
 
 @pytest.mark.parametrize("name", tg.TRAIN_CASES)
@@ -93,5 +95,16 @@ def test_dp2_step_vs_reference_shard_mean():
 @pytest.mark.parametrize("name", tg.TRAIN_CASES)
 def test_gpu_native_train_step_vs_reference(name):
     z, out = tg.replay(name, "cuda:0")
-    worst = tg.compare(z, out, **GPU_TOL)
-    print(name, "worst (grad rel, param abs, loss abs, buf rel):", worst)
+    rows = tg.compare_vs_f64(z, out, tg.replay_f64(name))
+    print(name, "per step (got, bound) for grad rel / param abs / loss abs / running-stat rel:", rows)
+    # the fp32 loss of the first step is the reference's within fp32 reassociation
+    assert abs(out["loss"][0] - float(z["loss"][0])) <= 1e-5
+
+
+def test_reference_fp32_vs_float64_conditioning():
+    """The fixtures' own fp32 steps against float64 (what the GPU bound scales): the
+    CPU restatement reproduces them exactly, so this documents their conditioning."""
+    for name in tg.TRAIN_CASES:
+        z = tg.load(name)
+        rows = tg.compare_vs_f64(z, None, tg.replay_f64(name), factor=1.0, floors=(1, 1, 1, 1))
+        assert rows

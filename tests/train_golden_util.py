@@ -58,6 +58,59 @@ def replay(name, device):
     return z, out
 
 
+def replay_f64(name):
+    """The same steps in float64 on CPU with torch.optim.SGD (the reference's math
+    without rounding): the yardstick for how far the reference's own fp32 step is
+    from exact, and for the GPU step."""
+    z = load(name)
+    cfg, m = build(z, "cpu")
+    m = m.double()
+    opt = torch.optim.SGD(m.parameters(), lr=float(z["lr"]), momentum=float(z["momentum"]),
+                          weight_decay=float(z["weight_decay"]), nesterov=bool(z["nesterov"]))
+    x = torch.from_numpy(z["x"]).double()
+    y = torch.from_numpy(z["y"])
+    out = dict(loss=[], g=[], p=[], b=[])
+    for _ in range(int(z["steps"])):
+        m.train()
+        opt.zero_grad()
+        loss = torch.nn.CrossEntropyLoss()(m(x), y)
+        loss.backward()
+        out["g"].append({k: p.grad.numpy().copy() for k, p in m.named_parameters()})
+        opt.step()
+        out["loss"].append(float(loss.item()))
+        out["p"].append({k: p.detach().numpy().copy() for k, p in m.named_parameters()})
+        out["b"].append({k: v.numpy().copy() for k, v in m.state_dict().items() if "running_" in k})
+    return out
+
+
+def _worst(z, out, f64, s):
+    """(grad rel, param abs, loss abs, buffer rel) of step s: out vs f64 (out=None: the fixture)."""
+    g = (lambda k: out["g"][s][k]) if out else (lambda k: z[f"g{s}__{k}"])
+    p = (lambda k: out["p"][s][k]) if out else (lambda k: z[f"p{s}__{k}"])
+    b = (lambda k: out["b"][s][k]) if out else (lambda k: z[f"b{s}__{k}"])
+    loss = out["loss"][s] if out else float(z["loss"][s])
+    return (max(rel_err(g(k), f64["g"][s][k]) for k in f64["g"][s]),
+            max(float(np.abs(p(k) - f64["p"][s][k]).max()) for k in f64["p"][s]),
+            abs(loss - f64["loss"][s]),
+            max(rel_err(b(k), f64["b"][s][k]) for k in f64["b"][s]))
+
+
+def compare_vs_f64(z, out, f64, factor=2.0, floors=(1e-4, 1e-6, 1e-5, 1e-5)):
+    """The step under test is at least as accurate as the reference's own fp32 step:
+    for every step and quantity, its distance from the float64 step is at most
+    `factor` x the reference's (floored: below the floors both are at rounding level).
+    Returns [(got, bound) per quantity] of the worst step."""
+    rows = []
+    for s in range(int(z["steps"])):
+        got, ref = _worst(z, out, f64, s), _worst(z, None, f64, s)
+        bound = [max(factor * r, f) for r, f in zip(ref, floors)]
+        rows.append(list(zip(got, bound)))
+        for (gv, bv), what in zip(rows[-1], ("grad", "param", "loss", "running stats")):
+            assert gv <= bv, (f"step {s} {what}: {gv:.3e} from float64 > bound {bv:.3e} "
+                              f"(reference fp32: {ref})")
+    return rows
+
+
 def rel_err(got, ref):
     """max |got - ref| / max |ref| (0 when both are 0)."""
     scale = float(np.abs(ref).max())
