@@ -264,7 +264,7 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model):
         act = H * W * CP * 4
     else:
         sp = 2 if prec == "bf16x3" else 1
-        fam = "block16_kernel" if os.environ.get("HONK_RES_ROWBAND") == "0" else "block16r_kernel"
+        fam = "block16r_kernel"
         kname = f"honk::res::{fam}<..., SP={sp}> (dilated 3x3 conv, bf16 MFMA{', 3 products' if sp == 2 else ''})"
         traffic = load_traffic(f"{fam}_sp{sp}", clips, model)
         act = H * W * CP * 2 * sp

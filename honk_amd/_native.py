@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("HONK_LIB", os.path.join(_HERE, "libhonk_hip.so"))  # HONK_LIB: experiment builds
+LIB_PATH = os.path.join(_HERE, "libhonk_hip.so")
 
 c_f32p = ctypes.c_void_p
 

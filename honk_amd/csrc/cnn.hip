@@ -147,21 +147,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
       for (int r = 0; r < 16; ++r) {
         const __bf16 h = (__bf16)xr[r];
         xh[r >> 3][r & 7] = h;
-#ifdef HONK_CNN_ABLATE_SPLIT
-        xl[r >> 3][r & 7] = h;
-#else
         xl[r >> 3][r & 7] = (__bf16)(xr[r] - (float)h);
-#endif
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const __bf16 h = (__bf16)wv[j];
         whv[j] = h;
-#ifdef HONK_CNN_ABLATE_SPLIT
-        wlv[j] = h;
-#else
         wlv[j] = (__bf16)(wv[j] - (float)h);
-#endif
       }
       *(cbf16x8*)&Xh[buf][0][mm][kq * 16] = xh[0];
       *(cbf16x8*)&Xh[buf][0][mm][kq * 16 + 8] = xh[1];
@@ -325,11 +317,8 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ 
 // Epilogue: bias + ReLU, NCHW fp32 stores (flatten order of model.py:194).
 // ---------------------------------------------------------------------------- //
 constexpr int C2X3_IMG = 96 * 1024;  // LDS bytes of one half image (PH*PW*128 <= this)
-// HONK_C2_ABLATE (timing-only experiment builds, wrong results): bit 1 no image
-// DMA, 2 every k-step loads k-step 0's weights, 4 no A-fragment reads
-#ifndef HONK_C2_ABLATE
-#define HONK_C2_ABLATE 0
-#endif
+// (ablations, round 1: no image DMA -10 %, no A-fragment reads -9 %, L1-resident
+// weights -5 %, all three -26 %)
 
 struct Conv2X3Args {
   const __bf16* in;    // [B][PH][PW][hi 64 | lo 64]
@@ -366,7 +355,6 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
   typedef uint4 AFr[MT][2];
   typedef uint4 WFr[2][2];
   auto loadA = [&](AFr& A, int delta) {
-    if constexpr (HONK_C2_ABLATE & 4) return;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int P = P0[m] + delta;
@@ -379,7 +367,7 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int pt = 0; pt < 2; ++pt) Wr[j][pt] = wl[(((HONK_C2_ABLATE & 2) ? 0 : s * 4 + j) * 2 + pt) * 64];
+      for (int pt = 0; pt < 2; ++pt) Wr[j][pt] = wl[((s * 4 + j) * 2 + pt) * 64];
   };
   f32x4 acc[MT][2];
   auto mma = [&](const AFr& A, const WFr& Wr) {
@@ -407,7 +395,7 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
       for (int j = 0; j < 2; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int h = 0; h < 2; ++h) {
       __syncthreads();  // every wave is done reading the previous image
-      for (int pc = wave; pc < ((HONK_C2_ABLATE & 1) ? 0 : pieces); pc += 4) {
+      for (int pc = wave; pc < pieces; pc += 4) {
         const int st = __builtin_amdgcn_readfirstlane(min(pc * 64, chunks - 64));
         const int L = st + lane;
         const int P = L >> 3, c = (L & 7) ^ (P & 7);
@@ -420,15 +408,6 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
       const int s0 = h * a.ntap;
       AFr A0, A1;
       WFr W0, W1;
-      if constexpr (HONK_C2_ABLATE & 4) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int pt = 0; pt < 2; ++pt) {
-            const unsigned v = 0x3f803f80u ^ (unsigned)(lane * 2654435761u + m * 40503u + pt);
-            A0[m][pt] = A1[m][pt] = uint4{v, v ^ 0x10001u, v ^ 0x20002u, v ^ 0x30003u};
-          }
-      }
       loadW(W0, s0);
       loadA(A0, 0);
       for (int t = 0; t < a.ntap; t += 2) {  // ntap even (host-checked)
@@ -499,9 +478,8 @@ __global__ void pack_conv2x3_kernel(const float* __restrict__ w, __bf16* __restr
 //   the lane with member 0 stores 4 channels' hi and lo runs (8 B each).
 // ---------------------------------------------------------------------------- //
 constexpr int C1X3_KH = 20, C1X3_KW = 8, C1X3_COLS = 32, C1X3_HMAX = 101;
-#ifndef HONK_C1_PREFETCH  // load the next clip's rows during this clip's MFMAs
-#define HONK_C1_PREFETCH 0  // measured 0.4% slower with it on (15 VGPR spills)
-#endif
+// (prefetching the next clip's rows during this clip's MFMAs measured 0.4 % slower:
+// 15 VGPR spills)
 constexpr int C1X3_PLANE = C1X3_HMAX * C1X3_COLS * 16;  // bytes of one (hi or lo) plane
 
 struct Conv1X3Args {
@@ -613,10 +591,9 @@ __global__ __launch_bounds__(512, 1) void conv1x3_kernel(Conv1X3Args a) {
       pv[n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, 0, 0));
     }
   };
-  if constexpr (HONK_C1_PREFETCH) fetch(blockIdx.x);
   for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
     __syncthreads();  // every wave is done with the previous clip's image
-    if constexpr (!HONK_C1_PREFETCH) fetch(b);
+    fetch(b);
 #pragma unroll
     for (int n = 0; n < NE; ++n) {
       const int e = tid + n * 512;
@@ -635,7 +612,6 @@ __global__ __launch_bounds__(512, 1) void conv1x3_kernel(Conv1X3Args a) {
       *(cbf16x8*)(img + C1X3_PLANE + slot) = l;
     }
     __syncthreads();
-    if constexpr (HONK_C1_PREFETCH) fetch(b + gridDim.x);
     __bf16* ob = a.out + (size_t)b * a.PH * a.PW * 128;
     AFr A0, A1;
     int mt = mg;

@@ -178,11 +178,6 @@ __device__ __forceinline__ void compute_stage(const float* cur, const int (&aoff
   stage_step<NT, MT, NDY, 0>(base, aoff, bcur, acc, a0, a1, wr, lane16, mid);
 }
 
-#ifdef HONK_STAMP
-// diagnostic build only: per-wave cycle split of the block kernels' main loops (s_memtime)
-__device__ unsigned long long honk_stamp_buf[256 * 16 * 8];
-#endif
-
 template <int NT, int MT, bool LAST>
 __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(BlockArgs a) {
   using G = Geo<NT, MT>;
@@ -263,16 +258,6 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
 
   int s = 0;
   f32x4 rv[MT];
-#ifdef HONK_STAMP
-  unsigned long long stamp32[7] = {0, 0, 0, 0, 0, 0, 0};
-  unsigned long long st32[8];
-#define HONK_STAMP32(x) (x) = __builtin_amdgcn_s_memtime()
-#define HONK_STAMP_VM(DY) { __builtin_amdgcn_s_waitcnt(0xc07f); stamp_vm += __builtin_amdgcn_s_memtime() - st32[2 * (DY)]; }
-  unsigned long long stamp_vm = 0;
-#else
-#define HONK_STAMP_VM(DY) ((void)0)
-#define HONK_STAMP32(x) ((void)0)
-#endif
   while (true) {
     f32x4 acc[MT];
 #pragma unroll
@@ -284,11 +269,8 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
   {                                                                                     \
     float* cur = smem + (s & 1) * G::BUF;                                               \
     float* nxt = smem + ((s + 1) & 1) * G::BUF;                                         \
-    HONK_STAMP32(st32[2 * DY]);                                                         \
     if (DY == 0) wait_vmcnt<G::VM_AFTER_GLDS_LAST>(); else wait_vmcnt<G::VM_AFTER_GLDS>(); \
-    HONK_STAMP_VM(DY);                                                                  \
     __builtin_amdgcn_s_barrier();                                                       \
-    HONK_STAMP32(st32[2 * DY + 1]);                                                     \
     auto mid = [&]() {                                                                  \
       if (DY < 2)                                                                       \
         issue_stage<NT, MT>(a, tile, DY + 1, nxt, wave, gpack);                         \
@@ -308,7 +290,6 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
     HONK_STAGE(1)
     HONK_STAGE(2)
 #undef HONK_STAGE
-    HONK_STAMP32(st32[6]);
 
     // epilogue: lane (g, i16) holds out channels c4..c4+3 of pixel i16 of each
     // m-tile: ReLU, residual add, pre-BN store (even layers) and BN store, 16 B
@@ -353,20 +334,9 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
         if (i16 == 0) *(f32x4*)(a.chsum + ((size_t)tile * MW + mg) * G::CP + c4) = csum;
       }
     }
-    HONK_STAMP32(st32[7]);
-#ifdef HONK_STAMP
-    for (int q = 0; q < 7; ++q) stamp32[q] += st32[q + 1] - st32[q];
-#endif
     tile += GR;
     if (tile >= a.ntiles) break;
   }
-#ifdef HONK_STAMP
-  if (lane == 0) {
-    unsigned long long* d = honk_stamp_buf + (size_t)(blockIdx.x * 16 + wave) * 8;
-    for (int q = 0; q < 7; ++q) d[q] = stamp32[q];
-    d[7] = stamp_vm + 1;
-  }
-#endif
 }
 
 // --------------------------------------------------------------------------- //
@@ -602,10 +572,10 @@ __global__ void copy_kernel(const float* __restrict__ src, float* __restrict__ d
 // host side
 // --------------------------------------------------------------------------- //
 struct Layout {
-  int C, CP, NT, L, NL, prec, KS16;
+  int C, CP, NT, L, NL, prec;
   int Hin, Win, H, W, ph, pw;
   size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, off_frag16, frag16_floats,
-      off_fragx3, fragx3_floats, off_fragr16, off_fragrx3, off_bias16, total;
+      off_fragx3, fragx3_floats, off_bias16, total;
 };
 
 static size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
@@ -639,19 +609,14 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   L->off_wout = L->off_bn + round64((size_t)2 * L->CP * L->L);
   L->off_bout = L->off_wout + round64((size_t)L->NL * L->C);
   L->off_zeros = L->off_bout + round64((size_t)L->NL);
-  // bf16 weight fragments per layer (layout G16::wfrag) for HONK_PREC_BF16 and the
-  // hi/lo pairs for HONK_PREC_BF16X3
-  L->KS16 = (6 * L->NT + 3) / 4;
+  // bf16 weight fragments per layer (layout G16R::xfrag: k-steps across the three
+  // dy rows) for HONK_PREC_BF16 and the hi/lo pairs for HONK_PREC_BF16X3
   L->off_frag16 = L->off_zeros + 64;
   L->frag16_floats = (size_t)g16_frag_bytes(L->NT, 1) / 4;
   L->off_fragx3 = L->off_frag16 + L->frag16_floats * L->L;
   L->fragx3_floats = (size_t)g16_frag_bytes(L->NT, 2) / 4;
-  // the same fragments in the row-band kernel's k order (k-steps run across the
-  // three dy rows: G16R::xfrag; same byte count)
-  L->off_fragr16 = L->off_fragx3 + L->fragx3_floats * L->L;
-  L->off_fragrx3 = L->off_fragr16 + L->frag16_floats * L->L;
   // folded input-BN bias [L][16 classes][CP] for the bf16 kernel
-  L->off_bias16 = L->off_fragrx3 + L->fragx3_floats * L->L;
+  L->off_bias16 = L->off_fragx3 + L->fragx3_floats * L->L;
   L->total = L->off_bias16 + (size_t)16 * L->CP * L->L;
   L->prec = d->precision;
   if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16 && L->prec != HONK_PREC_BF16X3)
@@ -696,64 +661,17 @@ static Plan plan_block(const Layout& L) {
   return best;
 }
 
-// bf16 kernel plan: 8 waves x MT m-tiles; MT is the largest whose 3-buffer ring
-// plus the layer's weights fit the 160 KiB LDS (SP = 1: NT = 3 -> 3, else 4;
-// SP = 2: NT = 3 -> 1, NT = 2 -> 2, NT = 1 -> 4)
-static Plan plan_block16(const Layout& L, int SP) {
-  int MT8 = 4;  // m-tiles per wave at 8 waves; the tile is 128 * MT8 pixels
-  while (MT8 > 1 && g16_lds_bytes(L.NT, 128 * MT8, SP) > 160 * 1024) --MT8;
-  const int MP = 128 * MT8;
-  const int thmax = MP / L.W;  // >= 1: make_layout bounds W
-  const int nb = (L.H + thmax - 1) / thmax;
-  const int th = (L.H + nb - 1) / nb;
-  return Plan{L.NT, MP / (16 * g16_nw(SP)), th, nb};
-}
-
-template <int NT, int MT, int SP>
-static int launch_block16(const Block16Args& a, hipStream_t st) {
-  using G = G16<NT, MT, SP>;
-  static_assert(G::LDS <= 160 * 1024, "LDS");
-  int grid = cu_count();
-  if (grid > a.ntiles) grid = a.ntiles;
-  const dim3 gd(grid), bd(G::NTHREADS);
-  if (a.chsum && a.res) hipLaunchKernelGGL((block16_kernel<NT, MT, SP, true, true>), gd, bd, 0, st, a);
-  else if (a.chsum) hipLaunchKernelGGL((block16_kernel<NT, MT, SP, true, false>), gd, bd, 0, st, a);
-  else if (a.res) hipLaunchKernelGGL((block16_kernel<NT, MT, SP, false, true>), gd, bd, 0, st, a);
-  else hipLaunchKernelGGL((block16_kernel<NT, MT, SP, false, false>), gd, bd, 0, st, a);
-  HONK_LAUNCH_CHECK("res block16_kernel");
-  return HONK_OK;
-}
-
-static int dispatch_block16(const Plan& p, int SP, const Block16Args& a, hipStream_t st) {
-  constexpr int B = HONK_B16_NW, X = HONK_X3_NW;
-  if (SP == 1) {
-    if (p.NT == 1 && p.MT == 32 / B) return launch_block16<1, 32 / B, 1>(a, st);
-    if (p.NT == 2 && p.MT == 32 / B) return launch_block16<2, 32 / B, 1>(a, st);
-    if (p.NT == 3 && p.MT == 24 / B) return launch_block16<3, 24 / B, 1>(a, st);
-  } else {
-    if (p.NT == 1 && p.MT == 32 / X) return launch_block16<1, 32 / X, 2>(a, st);
-    if (p.NT == 2 && p.MT == 16 / X) return launch_block16<2, 16 / X, 2>(a, st);
-    if (p.NT == 3 && p.MT == 8 / X) return launch_block16<3, 8 / X, 2>(a, st);
-  }
-  return fail(HONK_ERR_UNSUPPORTED, "no bf16 block kernel for NT=%d MT=%d SP=%d", p.NT, p.MT, SP);
-}
-
-// Row-band kernel plan (res_bf16r.inc): same (NT, MT) as plan_block16; TH rows of
+// Row-band kernel plan (res_bf16r.inc): 8 waves x MT m-tiles (g16r_mt); TH rows of
 // one dilation class per tile, limited by the tile's pixels and by the staging
-// image (TH + 2 rows); th = 0: not applicable (fall back to block16_kernel).
-// (3,3,1) (45-map bf16): 0.97 -> 0.89 ms per 4096-clip res15 launch vs the
-// per-dy-stage kernel (exp/ab_rowband.py); its LAST+RES variant spills 14 VGPRs.
-// HONK_RES_ROWBAND=0 selects the per-dy-stage kernel for A/B runs.
+// image (TH + 2 rows); TH = 0: the width does not fit the staging plan (the
+// bf16 / bf16x3 modes then fail with HONK_ERR_UNSUPPORTED; f32 has no such limit).
 struct PlanR {
   int NT, MT, TH;
 };
 static PlanR plan_block16r(const Layout& L, int SP) {
-  const Plan p = plan_block16(L, SP);
-  PlanR r{p.NT, p.MT, 0};
-  if (const char* e = getenv("HONK_RES_ROWBAND"))
-    if (atoi(e) == 0) return r;
-  const int MP = 16 * g16_nw(SP) * p.MT;
-  const int rpx = g16r_rpx(L.NT, MP / 128, SP);
+  PlanR r{L.NT, g16r_mt(L.NT, SP), 0};
+  const int MP = 16 * 8 * r.MT;
+  const int rpx = g16r_rpx(L.NT, r.MT, SP);
   int th = MP / L.W;
   if (rpx / L.W - 2 < th) th = rpx / L.W - 2;
   if (th < 1 || (th + 2) * L.W * L.CP * 2 * SP / 16 < 64) return r;
@@ -786,16 +704,14 @@ static int launch_block16r(const Block16RArgs& a, hipStream_t st) {
 }
 
 static int dispatch_block16r(const PlanR& p, int SP, const Block16RArgs& a, hipStream_t st) {
-  static_assert(HONK_B16_NW == 8 && !HONK_X3_WREG, "row-band kernel: 8-wave bf16 build, no WREG");
-  constexpr int X = 8 / HONK_X3_NW;  // m-tiles per wave scale with 8 / waves per workgroup
   if (SP == 1) {
-    if (p.NT == 1 && p.MT == 4) return launch_block16r<1, 4, 1>(a, st);
-    if (p.NT == 2 && p.MT == 4) return launch_block16r<2, 4, 1>(a, st);
-    if (p.NT == 3 && p.MT == 3) return launch_block16r<3, 3, 1>(a, st);
+    if (p.NT == 1 && p.MT == g16r_mt(1, 1)) return launch_block16r<1, g16r_mt(1, 1), 1>(a, st);
+    if (p.NT == 2 && p.MT == g16r_mt(2, 1)) return launch_block16r<2, g16r_mt(2, 1), 1>(a, st);
+    if (p.NT == 3 && p.MT == g16r_mt(3, 1)) return launch_block16r<3, g16r_mt(3, 1), 1>(a, st);
   } else {
-    if (p.NT == 1 && p.MT == 4 * X) return launch_block16r<1, 4 * X, 2>(a, st);
-    if (p.NT == 2 && p.MT == 2 * X) return launch_block16r<2, 2 * X, 2>(a, st);
-    if (p.NT == 3 && p.MT == 1 * X) return launch_block16r<3, 1 * X, 2>(a, st);
+    if (p.NT == 1 && p.MT == g16r_mt(1, 2)) return launch_block16r<1, g16r_mt(1, 2), 2>(a, st);
+    if (p.NT == 2 && p.MT == g16r_mt(2, 2)) return launch_block16r<2, g16r_mt(2, 2), 2>(a, st);
+    if (p.NT == 3 && p.MT == g16r_mt(3, 2)) return launch_block16r<3, g16r_mt(3, 2), 2>(a, st);
   }
   return fail(HONK_ERR_UNSUPPORTED, "no row-band kernel for NT=%d MT=%d SP=%d", p.NT, p.MT, SP);
 }
@@ -855,12 +771,14 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
   __bf16* R = (__bf16*)workspace;
   __bf16* X = R + act;
   float* chsum = (float*)(R + 2 * act);
-  const Plan p = plan_block16(L, SP);
   const PlanR pr = plan_block16r(L, SP);
   const double layer_flop_per_clip = 2.0 * L.H * L.W * L.C * L.C * 9;
   if (L.L == 0) return fail(HONK_ERR_UNSUPPORTED, "bf16 path needs n_layers >= 1");
+  if (pr.TH == 0)
+    return fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
+                "(use precision f32)", L.W);
   int rc;
-  if (pr.TH > 0) {
+  {
     // row-band kernel: tiles = (clip, dilation class, band of TH class rows)
     int nbc_last = 0;
     for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
@@ -874,8 +792,8 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         a.in = even ? X : R;
         a.res = even ? R : nullptr;
         a.out = (i == L.L) ? nullptr : (even ? R : X);
-        a.bfrag = (const uint4*)(SP == 2 ? packed + L.off_fragrx3 + (size_t)(i - 1) * L.fragx3_floats
-                                         : packed + L.off_fragr16 + (size_t)(i - 1) * L.frag16_floats);
+        a.bfrag = (const uint4*)(SP == 2 ? packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats
+                                         : packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
         a.bias = packed + L.off_bias16 + (size_t)16 * L.CP * (i - 1);
         a.chsum = (i == L.L) ? chsum : nullptr;
         a.H = L.H;
@@ -897,65 +815,12 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       }
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
-                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * g16_nw(SP), L.H * L.W, L.C, L.CP, L.NL,
+                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * 8 * pr.MT, L.H * L.W, L.C, L.CP, L.NL,
                          bn_last, bn_last + L.CP);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16 row-band)");
     }
     return HONK_OK;
   }
-  for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
-    const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
-    if ((int64_t)n * p.nbands > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
-    rc = (SP == 2) ? launch_conv0<__bf16, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
-                   : launch_conv0<__bf16, false>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
-    if (rc) return rc;
-    for (int i = 1; i <= L.L; ++i) {
-      const bool even = (i % 2) == 0;
-      Block16Args a;
-      a.in = even ? X : R;
-      a.res = even ? R : nullptr;
-      a.out = (i == L.L) ? nullptr : (even ? R : X);
-      a.bfrag = (const uint4*)(SP == 2 ? packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats
-                                       : packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
-      a.bias = packed + L.off_bias16 + (size_t)16 * L.CP * (i - 1);
-      a.chsum = (i == L.L) ? chsum : nullptr;
-      a.H = L.H;
-      a.W = L.W;
-      a.dil = d->use_dilation ? (1 << ((i - 1) / 3)) : 1;
-      a.TH = p.TH;
-      a.nbands = p.nbands;
-      a.ntiles = (int)(n * p.nbands);
-      TimedLaunch tl(st, layer_flop_per_clip * (double)n);
-      rc = dispatch_block16(p, SP, a, st);
-      tl.done(st);
-      if (rc) return rc;
-#ifdef HONK_STAMP
-      {
-        static unsigned long long h[256 * 8 * 8];
-        (void)hipStreamSynchronize(st);
-        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(honk_stamp_buf), sizeof(h));
-        double sum[8] = {0};
-        int nw = 0;
-        for (int w = 0; w < 256 * 8; ++w)
-          if (h[w * 8 + 7]) {
-            for (int q = 0; q < 7; ++q) sum[q] += (double)h[w * 8 + q];
-            sum[7] += (double)(h[w * 8 + 7] - 1);
-            ++nw;
-          }
-        if (nw)
-          fprintf(stderr, "stamp layer %d dil %d: w0 %.3f c0 %.3f w1 %.3f c1 %.3f w2 %.3f c2 %.3f (vmcnt %.3f) (of %.0f)\n",
-                  i, a.dil, sum[0] / sum[6], sum[1] / sum[6], sum[2] / sum[6], sum[3] / sum[6], sum[4] / sum[6],
-                  sum[5] / sum[6], sum[7] / sum[6], sum[6] / nw);
-      }
-#endif
-    }
-    const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
-    hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
-                       packed + L.off_bout, logits + c0 * L.NL, p.nbands * g16_nw(SP), L.H * L.W, L.C, L.CP, L.NL,
-                       bn_last, bn_last + L.CP);
-    HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16)");
-  }
-  return HONK_OK;
 }
 
 }  // namespace res
@@ -978,14 +843,14 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   const int64_t ch = chunk_clips(L, batch);
   if (L.prec != HONK_PREC_F32) {
     const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;
-    const Plan p = plan_block16(L, SP);
     const PlanR pr = plan_block16r(L, SP);
-    int nb = p.nbands;
-    if (pr.TH > 0) {
-      const int nr = max_bands_per_clip(L, pr.TH, d->use_dilation);
-      if (nr > nb) nb = nr;
+    if (pr.TH == 0) {
+      fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
+           "(use precision f32)", L.W);
+      return 0;
     }
-    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * nb * g16_nw(SP) * L.CP * sizeof(float);
+    const int nb = max_bands_per_clip(L, pr.TH, d->use_dilation);
+    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * nb * 8 * pr.MT * L.CP * sizeof(float);
   }
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
@@ -1014,15 +879,11 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
     // bf16: the input BatchNorm (layer i-1's; none for layer 1) folded into
     // the weights and the border-class bias; layer i-1's BN was packed above
     const float* in_bn = (i > 0) ? packed + L.off_bn + (size_t)2 * L.CP * (i - 1) : nullptr;
-    const int n16 = 3 * L.KS16 * L.NT * 64 * 8;
+    const int n16 = ((18 * L.NT + 3) / 4) * L.NT * 64 * 8;
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
-                       (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16, 1, 0);
+                       (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, 1);
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
-                       (__bf16*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, L.KS16, 2, 0);
-    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
-                       (__bf16*)(packed + L.off_fragr16 + (size_t)i * L.frag16_floats), L.C, L.NT, L.KS16, 1, 1);
-    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
-                       (__bf16*)(packed + L.off_fragrx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, L.KS16, 2, 1);
+                       (__bf16*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, 2);
     HONK_LAUNCH_CHECK("pack_block16");
     hipLaunchKernelGGL(pack_bias16_kernel, dim3(cdiv(16 * L.CP, 256)), dim3(256), 0, st, t[1 + i],
                        in_bn ? in_bn + L.CP : nullptr, packed + L.off_bias16 + (size_t)16 * L.CP * i, L.C, L.CP);
@@ -1090,26 +951,6 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
       rc = dispatch_block(p, a, st);
       tl.done(st);
       if (rc) return rc;
-#ifdef HONK_STAMP
-      {
-        static unsigned long long h[256 * 16 * 8];
-        (void)hipStreamSynchronize(st);
-        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(honk_stamp_buf), sizeof(h));
-        double sum[8] = {0};
-        int nw = 0;
-        for (int w = 0; w < 256 * 16; ++w)
-          if (h[w * 8 + 7]) {
-            double tot = 0;
-            for (int q = 0; q < 7; ++q) tot += (double)h[w * 8 + q];
-            for (int q = 0; q < 7; ++q) sum[q] += (double)h[w * 8 + q] / tot;
-            sum[7] += (double)(h[w * 8 + 7] - 1) / tot;
-            ++nw;
-          }
-        if (nw)
-          fprintf(stderr, "stamp32 layer %d: w0 %.3f c0 %.3f w1 %.3f c1 %.3f w2 %.3f c2 %.3f epi %.3f (vmcnt part of waits %.3f)\n", i,
-                  sum[0] / nw, sum[1] / nw, sum[2] / nw, sum[3] / nw, sum[4] / nw, sum[5] / nw, sum[6] / nw, sum[7] / nw);
-      }
-#endif
     }
     if (L.L == 0) {  // no block layer: mean of the conv0 output
       hipLaunchKernelGGL(tail_kernel, dim3((unsigned)n), dim3(L.CP * (256 / L.CP)), 0, st, R,

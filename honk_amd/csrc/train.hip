@@ -73,10 +73,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
 // 4 per ds_read_b128).  d = 1 is the plain band of TH rows.
 // ---------------------------------------------------------------------------- //
 constexpr int TC_XL = 64 * 1024;  // bytes of the staged input tile (wgrad: and of its dy tile)
-#ifndef HONK_TC_XLC
-#define HONK_TC_XLC (64 * 1024)
-#endif
-constexpr int TC_XLC = HONK_TC_XLC;  // conv3x3_kernel's input tile (19 maps); 96 KB = whole clips, 4 px/thread, 1 block/CU: 23 % slower step
+constexpr int TC_XLC = 64 * 1024;  // conv3x3_kernel's input tile (19 maps); 96 KB = whole clips, 4 px/thread, 1 block/CU: 23 % slower step
 
 template <int C>
 struct TC {

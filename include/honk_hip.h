@@ -15,9 +15,16 @@
  * Conventions: every pointer named x/logits/packed/tensors[i]/workspace is a
  * DEVICE pointer (hipMalloc / torch caching allocator); `stream` is a
  * hipStream_t passed as void*.  Work is enqueued on `stream`; no call
- * synchronises, allocates device memory or keeps global mutable state besides a
- * thread-local last-error string.  Status: 0 = ok, <0 = error, see
- * honk_last_error().  All arithmetic is IEEE fp32 (fp32 MFMA / FMA).
+ * synchronises or allocates device memory.  Global state: a thread-local
+ * last-error string, a per-device CU-count cache, and the mutex-guarded
+ * timing window of honk_timing_enable/read (off unless enabled; a diagnostic,
+ * not used by the forward itself).  Status: 0 = ok, <0 = error, see
+ * honk_last_error().
+ * Arithmetic: fp32 inputs/outputs everywhere; the res and cnn forwards take a
+ * precision field (HONK_PREC_F32: IEEE fp32 MFMA; HONK_PREC_BF16X3: fp32 values
+ * as bf16 hi + lo pairs, 3 bf16 MFMA products per MAC, fp32 accumulation -- both
+ * meet the 1e-4 logit bar; HONK_PREC_BF16: bf16, top-1 parity); every other
+ * entry point is IEEE fp32 (MFMA / FMA), the BatchNorm statistics fp64.
  */
 #ifndef HONK_HIP_H
 #define HONK_HIP_H
@@ -48,7 +55,10 @@ typedef struct honk_res_desc {
                              accumulate; top-1 parity) or HONK_PREC_BF16X3
                              (fp32 values as bf16 hi + lo pairs, products
                              hi*hi + hi*lo + lo*hi on bf16 MFMA, fp32
-                             accumulate; 1e-4 parity) -- same packed buffer  */
+                             accumulate; 1e-4 parity) -- same packed buffer.
+                             BF16 / BF16X3: the row-band staging plan bounds
+                             the (pooled) width -- 66 for 45-map bf16x3, 154
+                             for 45-map bf16 -- HONK_ERR_UNSUPPORTED beyond */
 } honk_res_desc;
 
 #define HONK_PREC_F32 0

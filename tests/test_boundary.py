@@ -176,12 +176,17 @@ def test_abi_queries_without_gpu():
     assert n >= 45 * 9 + 13 * 9 * 48 * 48
     assert lib.honk_res_workspace_bytes(d, 10) == 3 * 10 * 101 * 40 * 48 * 4 + 10 * 13 * 4 * 48 * 4
     # bf16: two pre-BN bf16 activation buffers (residual stream + odd-layer output)
-    # + per-(tile, wave) channel sums of the last layer; row-band kernel: res15 tiles of
-    # 9 rows of one dilation class (8 waves x 3 m-tiles), at most 16 per clip (dilation 16:
-    # 16 classes of 6-7 rows, one tile each)
+    # + per-(tile, wave, m-tile) channel sums of the last layer; row-band kernel: res15
+    # tiles of 9 rows of one dilation class (8 waves x 3 m-tiles), at most 16 per clip
+    # (dilation 16: 16 classes of 6-7 rows, one tile each)
     d16 = _native.ResDesc(n_labels=12, n_maps=45, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
                           height=101, width=40, precision=_native.PRECISIONS["bf16"])
-    assert lib.honk_res_workspace_bytes(d16, 10) == 2 * 10 * 101 * 40 * 48 * 2 + 10 * 16 * 8 * 48 * 4
+    assert lib.honk_res_workspace_bytes(d16, 10) == 2 * 10 * 101 * 40 * 48 * 2 + 10 * 16 * 8 * 3 * 48 * 4
+    # bf16x3 past the row-band plan's width: 0 bytes and the reason in honk_last_error
+    wide = _native.ResDesc(n_labels=12, n_maps=45, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
+                           height=101, width=67, precision=_native.PRECISIONS["bf16x3"])
+    assert lib.honk_res_workspace_bytes(wide, 10) == 0
+    assert b"row-band staging plan" in lib.honk_last_error()
     bad = _native.ResDesc(n_labels=12, n_maps=64, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
                           height=101, width=40)
     assert lib.honk_res_packed_floats(bad) == 0

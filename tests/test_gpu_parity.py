@@ -202,3 +202,48 @@ def test_linear_small_n_abi(m, k, n, relu):
     if relu:
         ref = torch.relu(ref)
     torch.testing.assert_close(y[:m].cpu(), ref, atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("prec", ["f32", "bf16x3"])
+def test_c2_full_batch_cnn_trad_pool2(prec):
+    """Config C2 at its full size (65,536 clips in one call, 22 internal chunks of
+    ~3,100 clips): the batch equals the same clips run as pieces that straddle the
+    chunk boundaries (bitwise), and sampled clips -- first, last, both sides of
+    chunk boundaries -- match the float64 oracle at the 1e-4 bar."""
+    name = "cnn-trad-pool2"
+    cfg = dict(ref_configs()[name])
+    params = orc.make_params(cfg, 65)
+    m = module(cfg, params, name)
+    m.honk_precision = prec
+    g = torch.Generator(device=DEV).manual_seed(65536)
+    x = torch.randn(65536, 101, 40, device=DEV, generator=g)
+    with torch.no_grad():
+        full = m(x)
+        cuts = [0, 3000, 3210, 9000, 31000, 65535, 65536]
+        parts = torch.cat([m(x[a:b]) for a, b in zip(cuts, cuts[1:])])
+    assert torch.equal(full, parts)
+    idx = [0, 1, 3099, 3100, 3101, 3102, 3103, 3104, 6205, 6206, 32768, 65534, 65535]
+    np.testing.assert_allclose(full[idx].cpu().numpy(), orc.forward(params, cfg, x[idx].cpu().numpy()),
+                               atol=ATOL, rtol=0)
+
+
+@pytest.mark.parametrize("width,prec,ok", [(66, "bf16x3", True), (67, "bf16x3", False), (80, "bf16", True),
+                                           (160, "bf16", False), (160, "f32", True)])
+def test_res_wide_input_envelope(width, prec, ok):
+    """The row-band bf16 / bf16x3 kernel stages (TH + 2) full rows: inputs wider than
+    its LDS plan (66 px for 45-map bf16x3, 154 for bf16) fail loudly; f32 has no
+    such limit.  Inside the envelope the logits match the oracle (1e-4 for the
+    fp32-parity modes, top-1-mode tolerance for bf16)."""
+    cfg = dict(ref_configs()["res15"], n_layers=4)
+    rng = np.random.Generator(np.random.PCG64(width))
+    params = orc.make_params(cfg, width)
+    x = rng.standard_normal((2, 101, width)).astype(np.float32)
+    params = orc.calibrate_bn(params, cfg, x)
+    m = module(cfg, params, "res15")
+    m.honk_precision = prec
+    if not ok:
+        with pytest.raises(RuntimeError, match="row-band staging plan"):
+            run(m, x)
+        return
+    tol = 5e-2 if prec == "bf16" else ATOL
+    np.testing.assert_allclose(run(m, x), orc.forward(params, cfg, x), atol=tol, rtol=0)

@@ -55,7 +55,7 @@ def main():
     # per kernel family (all template instances, weighted by launches) -> the
     # profiles/pmc_<family>.json that bench.py reads for roofline.traffic
     def family(k):
-        for fam in ("block16_kernel", "block16r_kernel"):  # split by SP (3rd template argument): sp1 = bf16, sp2 = bf16x3
+        for fam in ("block16r_kernel",):  # split by SP (3rd template argument): sp1 = bf16, sp2 = bf16x3
             if f"::{fam}<" in k:
                 return f"{fam}_sp" + k.split("<")[1].split(",")[2].strip()
         for fam in ("block_kernel", "conv_gemm_kernel"):
