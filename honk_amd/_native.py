@@ -79,11 +79,13 @@ _lib = None
 _lock = threading.Lock()
 
 
-def load(path: str = LIB_PATH):
-    """Load (once) and return the ctypes library; raise RuntimeError if unavailable."""
+def load(path: str = None):
+    """Load (once) and return the ctypes library; raise RuntimeError if unavailable.
+    ``HONK_LIB`` names an alternative build of the library (experiment builds)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("HONK_LIB") or LIB_PATH
     with _lock:
         if _lib is not None:
             return _lib

@@ -353,7 +353,9 @@ __device__ __forceinline__ void store4(__bf16* o, f32x4 v) {
 // pixels x CP channels are staged in LDS and written back as one contiguous
 // span with 16-byte accesses (a direct thread-per-pixel store strides 8-16 B
 // accesses by the pixel pitch).  The packed weights are zero for channels >= C.
-template <int PH, int PW, typename OT, bool SPLIT>
+// ONES: channel C (< CP) holds 1.0 -- the bias channel of the weight-stationary
+// bf16 kernels (pack_block16_kernel)
+template <int PH, int PW, typename OT, bool SPLIT, bool ONES>
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, OT* __restrict__ out,
                                                     const float* __restrict__ w0, int n, int Hin,
                                                     int Win, int H, int W, int C, int CP) {
@@ -403,6 +405,7 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
             s += fmaxf(acc, 0.f);
           }
         v[u] = (PH * PW > 1) ? s * inv : s;
+        if (ONES && c4 + u == C) v[u] = 1.f;
       }
       const f32x4 vv = {v[0], v[1], v[2], v[3]};
       store4(o + c4, vv);
@@ -520,6 +523,7 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 
 #include "res_bf16.inc"
 #include "res_bf16r.inc"
+#include "res_bf16w.inc"
 
 // --------------------------------------------------------------------------- //
 // weight packing
@@ -687,6 +691,100 @@ static int max_bands_per_clip(const Layout& L, int TH, int use_dilation) {
   return best;
 }
 
+// Weight-stationary kernel plan (res_bf16w.inc) for one layer at dilation d: the
+// band height TH (class rows per tile) minimising a cycle model -- per tile, the
+// slowest wave's m-tiles x the MFMA cycles of one m-tile plus a fixed per-tile
+// cost (barrier, first operand reads) -- among the heights whose (TH + 2)-row
+// image (W + d pixels per row + 1) fits the staging buffer.  0: does not fit.
+static int plan_w_th(const Layout& L, int SP, int d) {
+  const int imgpx = g16w_img_px(L.NT, SP);
+  const int RW = L.W + d;
+  int thmax = (imgpx - 1) / RW - 2;
+  const int q = L.H / d, rem = L.H - q * d;
+  const int nmax = q + (rem ? 1 : 0);
+  if (thmax > nmax) thmax = nmax;
+  if (thmax < 1) return 0;
+  // 16-bit per-lane offsets of the kernel (tap offsets, staging chunks in 16-B
+  // units, the separator code 0xffff landing past the clip)
+  const long CB = 32L * L.NT * SP, RB = (long)L.W * CB;
+  if ((RW + 1) * CB + 16 * (2 * L.NT) >= 32768) return 0;
+  if (0xffffL * 16 - (long)d * RB < (long)L.H * RB) return 0;
+  while (thmax >= 1 && ((long)(thmax + 1) * d * RB + RB) / 16 >= 0xffff) --thmax;
+  if (thmax < 1) return 0;
+  const int ksa = (18 * L.NT + 3) / 4;
+  const double c_mt = ksa * L.NT * (SP == 2 ? 3 : 1) * 16.0, c_tile = 1500.0;
+  int best = 0;
+  double best_cost = 1e300;
+  for (int th = thmax; th >= 1; --th) {
+    double cost = 0;
+    for (int cls = 0; cls < d; ++cls) {
+      const int n = q + (cls < rem ? 1 : 0);
+      for (int k = 0; k * th < n; ++k) {
+        const int rows = std::min(th, n - k * th);
+        const int nmt = (rows * L.W + 15) / 16;
+        const int it = std::max(1, (nmt + 3) / 4);
+        cost += it * c_mt + c_tile;
+      }
+    }
+    if (cost < best_cost * (1 - 1e-9)) {
+      best_cost = cost;
+      best = th;
+    }
+  }
+  return best;
+}
+static int dil_of(const honk_res_desc* d, int i) { return d->use_dilation ? (1 << ((i - 1) / 3)) : 1; }
+// bands per clip of layer i under the weight-stationary plan (0: a layer does not fit)
+static int bands_w(const Layout& L, const honk_res_desc* d, int SP, int i) {
+  const int dl = dil_of(d, i);
+  const int th = plan_w_th(L, SP, dl);
+  return th ? band_geo(L.H, dl, th).nbc : 0;
+}
+// Which bf16 / bf16x3 block kernel runs: the weight-stationary one where it was
+// measured faster (45 maps at bf16x3: res15 2.14 vs 2.21 ms per 4096-clip
+// launch; it loses 7-20 % on the narrow, pooled and bf16 configurations), the
+// row-band one elsewhere.  HONK_RES_KERNEL=w / r forces either (tests run both).
+static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
+  bool want = L.NT == 3 && SP == 2;
+  if (const char* e = getenv("HONK_RES_KERNEL")) {
+    if (e[0] == 'r') return false;
+    if (e[0] == 'w') want = true;
+  }
+  if (!want) return false;
+  if (L.W >= 64) return false;  // m-tile walk steps 64 pixels = at most one row carry
+  if (L.C >= L.CP) return false;  // no zero-padding channel for the folded bias
+  if (L.ph * L.pw > 1 && !((L.ph == 2 && L.pw == 2) || (L.ph == 4 && L.pw == 3))) return false;  // conv0 shapes
+  for (int i = 1; i <= L.L; ++i)
+    if (!bands_w(L, d, SP, i)) return false;
+  return true;
+}
+
+template <int NT, int SP>
+static int launch_block16w(const Block16WArgs& a, hipStream_t st) {
+  int grid = cu_count();
+  if (grid > a.ntiles) grid = a.ntiles;
+  const dim3 gd(grid), bd(G16W<NT, SP>::NTHREADS);
+  const bool last = a.chsum != nullptr, res = a.res != nullptr;
+  if (last && res) hipLaunchKernelGGL((block16w_kernel<NT, SP, true, true>), gd, bd, 0, st, a);
+  else if (last) hipLaunchKernelGGL((block16w_kernel<NT, SP, true, false>), gd, bd, 0, st, a);
+  else if (res) hipLaunchKernelGGL((block16w_kernel<NT, SP, false, true>), gd, bd, 0, st, a);
+  else hipLaunchKernelGGL((block16w_kernel<NT, SP, false, false>), gd, bd, 0, st, a);
+  HONK_LAUNCH_CHECK("res block16w_kernel");
+  return HONK_OK;
+}
+static int dispatch_block16w(int NT, int SP, const Block16WArgs& a, hipStream_t st) {
+  if (SP == 1) {
+    if (NT == 1) return launch_block16w<1, 1>(a, st);
+    if (NT == 2) return launch_block16w<2, 1>(a, st);
+    if (NT == 3) return launch_block16w<3, 1>(a, st);
+  } else {
+    if (NT == 1) return launch_block16w<1, 2>(a, st);
+    if (NT == 2) return launch_block16w<2, 2>(a, st);
+    if (NT == 3) return launch_block16w<3, 2>(a, st);
+  }
+  return fail(HONK_ERR_UNSUPPORTED, "no weight-stationary kernel for NT=%d SP=%d", NT, SP);
+}
+
 template <int NT, int MT, int SP>
 static int launch_block16r(const Block16RArgs& a, hipStream_t st) {
   using G = G16<NT, MT, SP>;
@@ -739,21 +837,21 @@ static int dispatch_block(const Plan& p, const BlockArgs& a, hipStream_t st) {
   return fail(HONK_ERR_UNSUPPORTED, "no block kernel for NT=%d MT=%d", p.NT, p.MT);
 }
 
-template <typename OT, bool SPLIT = false>
+template <typename OT, bool SPLIT = false, bool ONES = false>
 static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w0, int64_t n,
                         hipStream_t st) {
   const int64_t total = n * L.H * L.W;
   const int blocks = (int)cdiv(total, 256);
 #define HONK_C0(PH, PW)                                                                               \
   if (L.ph == PH && L.pw == PW) {                                                                     \
-    hipLaunchKernelGGL((conv0_kernel<PH, PW, OT, SPLIT>), dim3(blocks), dim3(256), 0, st, x, out, w0, \
+    hipLaunchKernelGGL((conv0_kernel<PH, PW, OT, SPLIT, ONES>), dim3(blocks), dim3(256), 0, st, x, out, w0, \
                        (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                                    \
     HONK_LAUNCH_CHECK("res conv0_kernel");                                                            \
     return HONK_OK;                                                                                   \
   }
   HONK_C0(1, 1) HONK_C0(2, 2) HONK_C0(4, 3)
 #undef HONK_C0
-  if (SPLIT) return fail(HONK_ERR_UNSUPPORTED, "bf16x3: avg-pool %dx%d has no conv0 kernel", L.ph, L.pw);
+  if (SPLIT || ONES) return fail(HONK_ERR_UNSUPPORTED, "bf16: avg-pool %dx%d has no conv0 kernel", L.ph, L.pw);
   hipLaunchKernelGGL((conv0_generic_kernel<OT>), dim3(blocks), dim3(256), 0, st, x, out, w0, (int)n, L.Hin,
                      L.Win, L.H, L.W, L.C, L.CP, L.ph, L.pw);
   HONK_LAUNCH_CHECK("res conv0_generic_kernel");
@@ -778,6 +876,50 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
     return fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
                 "(use precision f32)", L.W);
   int rc;
+  if (use_w_kernel(L, d, SP)) {
+    // weight-stationary kernel: tiles = (clip, dilation class, band of TH class rows), TH per dilation
+    int nbc_last = 0;
+    for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
+      const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
+      rc = (SP == 2) ? launch_conv0<__bf16, true, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+                     : launch_conv0<__bf16, false, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+      if (rc) return rc;
+      for (int i = 1; i <= L.L; ++i) {
+        const bool even = (i % 2) == 0;
+        Block16WArgs a;
+        a.in = even ? X : R;
+        a.res = even ? R : nullptr;
+        a.out = (i == L.L) ? nullptr : (even ? R : X);
+        a.wfrag = (const char*)(SP == 2 ? packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats
+                                        : packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
+        a.chsum = (i == L.L) ? chsum : nullptr;
+        a.H = L.H;
+        a.W = L.W;
+        a.dil = dil_of(d, i);
+        a.TH = plan_w_th(L, SP, a.dil);
+        const BandGeo bg = band_geo(L.H, a.dil, a.TH);
+        a.nbc = bg.nbc;
+        a.rem = bg.rem;
+        a.nb1 = bg.nb1;
+        a.nb0 = bg.nb0;
+        a.lgd = 0;
+        while ((1 << a.lgd) < a.dil) ++a.lgd;
+        if ((int64_t)n * a.nbc > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
+        a.ntiles = (int)(n * a.nbc);
+        if (i == L.L) nbc_last = a.nbc;
+        TimedLaunch tl(st, layer_flop_per_clip * (double)n);
+        rc = dispatch_block16w(L.NT, SP, a, st);
+        tl.done(st);
+        if (rc) return rc;
+      }
+      const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
+      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * 4, L.H * L.W, L.C, L.CP, L.NL,
+                         bn_last, bn_last + L.CP);
+      HONK_LAUNCH_CHECK("res tail_sum_kernel (weight-stationary)");
+    }
+    return HONK_OK;
+  }
   {
     // row-band kernel: tiles = (clip, dilation class, band of TH class rows)
     int nbc_last = 0;
@@ -850,7 +992,12 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
       return 0;
     }
     const int nb = max_bands_per_clip(L, pr.TH, d->use_dilation);
-    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * nb * 8 * pr.MT * L.CP * sizeof(float);
+    size_t parts = (size_t)nb * 8 * pr.MT;  // row-band kernel: [tile][wave][m-tile] channel sums
+    if (L.L > 0 && use_w_kernel(L, d, SP)) {
+      const size_t pw = (size_t)bands_w(L, d, SP, L.L) * 4;  // weight-stationary: [tile][wave]
+      if (pw > parts) parts = pw;
+    }
+    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * parts * L.CP * sizeof(float);
   }
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
@@ -880,9 +1027,11 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
     // the weights and the border-class bias; layer i-1's BN was packed above
     const float* in_bn = (i > 0) ? packed + L.off_bn + (size_t)2 * L.CP * (i - 1) : nullptr;
     const int n16 = ((18 * L.NT + 3) / 4) * L.NT * 64 * 8;
-    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
+    const float* in_shift = in_bn ? in_bn + L.CP : nullptr;
+    const int odd = ((i + 1) & 1);  // layer i + 1 (1-based) is odd
+    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn, in_shift, odd,
                        (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, 1);
-    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn,
+    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn, in_shift, odd,
                        (__bf16*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, 2);
     HONK_LAUNCH_CHECK("pack_block16");
     hipLaunchKernelGGL(pack_bias16_kernel, dim3(cdiv(16 * L.CP, 256)), dim3(256), 0, st, t[1 + i],

@@ -1,0 +1,106 @@
+"""Both bf16 / bf16x3 res block kernels on every shape, whichever the default
+dispatch picks: the row-band kernel (block16r_kernel, weights in LDS, border
+bias table) and the weight-stationary kernel (block16w_kernel, weights in the
+register file, folded-BN bias in the zero-padding channel C), forced with
+HONK_RES_KERNEL.  bf16x3: the fp32 parity bar (1e-4 absolute) vs the float64
+oracle and the reference's golden logits; bf16: the top-1 bar of test_gpu_bf16.
+The two kernels must also agree with each other."""
+import numpy as np
+import pytest
+import torch
+
+from honk_amd import _native
+from honk_amd import model as hm
+from oracle import ref_numpy as orc
+from golden_util import fixture_names, load_fixture, ref_configs
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+KERNELS = ("w", "r")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _native.load()
+
+
+def _module(cfg, params, name, prec):
+    m = hm.find_model(name)(cfg)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    m = m.eval().to(DEV)
+    m.honk_precision = prec
+    return m
+
+
+def _run(m, x):
+    with torch.no_grad():
+        out = m(torch.as_tensor(x).to(DEV))
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def _case(cfg, B, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    params = orc.make_params(cfg, seed)
+    params = orc.calibrate_bn(params, cfg, rng.standard_normal((2, 101, 40)).astype(np.float32), seed=seed)
+    return params, rng.standard_normal((B, 101, 40)).astype(np.float32)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("name", [n for n in fixture_names() if n.startswith("res")])
+def test_bf16x3_golden_both_kernels(monkeypatch, kernel, name):
+    monkeypatch.setenv("HONK_RES_KERNEL", kernel)
+    cfg, params, x, logits, meta = load_fixture(name)
+    out = _run(_module(cfg, params, meta["model"], "bf16x3"), x)
+    np.testing.assert_allclose(out, logits, atol=1e-4, rtol=0)
+
+
+# shapes the weight-stationary kernel specialises on: 1 .. 3 out-channel tiles
+# (the merged half-used last k-step at 1 and 3), pooled widths 13 and 20, the
+# dilated family, odd and even last layers (plain / residual epilogue)
+SHAPES = [("res8", dict(n_feature_maps=1)), ("res8", dict(n_feature_maps=5)), ("res8", dict(n_feature_maps=15)),
+          ("res8", dict(n_feature_maps=19)), ("res8", dict(n_feature_maps=31)), ("res8", dict(n_feature_maps=45)),
+          ("res8", dict(n_layers=1)), ("res8", dict(n_layers=2)), ("res26", dict(n_layers=5)),
+          ("res15", dict(n_layers=7)), ("res15", dict(n_layers=13, n_feature_maps=33)),
+          ("res15-narrow", dict(n_layers=4)), ("res15", dict(use_dilation=False, n_layers=3))]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("name,override", SHAPES)
+def test_bf16x3_shapes_both_kernels(monkeypatch, kernel, name, override):
+    monkeypatch.setenv("HONK_RES_KERNEL", kernel)
+    cfg = dict(ref_configs()[name])
+    cfg.update(override)
+    params, x = _case(cfg, 3, seed=17)
+    out = _run(_module(cfg, params, name, "bf16x3"), x)
+    np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("name,override", SHAPES)
+def test_bf16_shapes_kernels_agree(monkeypatch, name, override):
+    """bf16: both kernels within the bf16 bar of the oracle and of each other
+    (they round the same products in a different order)."""
+    cfg = dict(ref_configs()[name])
+    cfg.update(override)
+    params, x = _case(cfg, 16, seed=23)
+    ref = orc.forward(params, cfg, x)
+    outs = {}
+    for k in KERNELS:
+        monkeypatch.setenv("HONK_RES_KERNEL", k)
+        outs[k] = _run(_module(cfg, params, name, "bf16"), x)
+        assert np.abs(outs[k] - ref).max() <= 0.05
+        assert np.mean(outs[k].argmax(1) == ref.argmax(1)) >= 0.9
+    assert np.abs(outs["w"] - outs["r"]).max() <= 0.05
+
+
+def test_w_kernel_batch_invariance(monkeypatch):
+    monkeypatch.setenv("HONK_RES_KERNEL", "w")
+    cfg = dict(ref_configs()["res15"])
+    params, x = _case(cfg, 11, seed=5)
+    m = _module(cfg, params, "res15", "bf16x3")
+    full = _run(m, x)
+    assert np.array_equal(full, np.concatenate([_run(m, x[:4]), _run(m, x[4:])]))
+    monkeypatch.setenv("HONK_RES_CHUNK", "3")
+    assert np.array_equal(full, _run(m, x))
