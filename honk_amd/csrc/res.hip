@@ -524,6 +524,7 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 #include "res_bf16.inc"
 #include "res_bf16r.inc"
 #include "res_bf16w.inc"
+#include "res_bf16p.inc"
 
 // --------------------------------------------------------------------------- //
 // weight packing
@@ -759,6 +760,77 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
   return true;
 }
 
+// Fused pair plan (res_bf16p.inc) for layers A (dilation d) and B (tap stride sB
+// class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
+// an exact walk over the steps of the longest stream.  ok = false: does not fit.
+struct PairPlan {
+  bool ok;
+  int lag, NRA, NRB, slotb, ppr;
+};
+static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw) {
+  PairPlan pp{false, 0, 0, 0, 0, 0};
+  const int P = 64, W = L.W, H = L.H;
+  const long CB = 32L * L.NT * SP;
+  pp.ppr = (int)((W * CB + 1023) / 1024);
+  pp.slotb = pp.ppr * 1024;
+  const long total = (long)cpw * H * W, rows_total = (long)cpw * H;
+  if (total >= (1L << 24) || sB < 1 || sB > 2) return pp;
+  auto rho = [&](long q) { return q / W; };
+  auto F = [&](long k) {
+    long lp = (k + 2) * P + 32;
+    lp = (lp < total ? lp : total) - 1;
+    const long f = rho(lp) + 1;
+    return f < rows_total - 1 ? f : rows_total - 1;
+  };
+  // B at step k computes [kP - lag - P, kP - lag) and prefetches the next step's
+  // first 32 pixels; everything it reads must be finished by A before the step's
+  // barrier: A's pixels below (k - 1) P + 32 (A's last m-tiles defer their
+  // epilogue into the next step)
+  int lag = -1;
+  for (int cand = 0; cand <= 2048 && lag < 0; cand += 16) {
+    const long ns = (total + cand + P - 1) / P + 1;
+    bool ok = true;
+    for (long k = 0; k < ns && ok; ++k) {
+      long lo = k * P - cand - P, hi = k * P - cand + 32;
+      if (lo < 0) lo = 0;
+      if (hi > total) hi = total;
+      if (hi <= lo) continue;
+      const long done = (k - 1) * P + 32;
+      if (done >= total) continue;
+      long rmax = rho(hi - 1) + sB;
+      if (rmax > rows_total - 1) rmax = rows_total - 1;
+      if ((rmax + 1) * W > done) ok = false;
+    }
+    if (ok) lag = cand;
+  }
+  if (lag < 0) return pp;
+  pp.lag = lag;
+  const long ns = (total + lag + P - 1) / P + 1;
+  long nra = 0, nrb = 0;
+  for (long k = 0; k < ns; ++k) {
+    if (k * P < total) {  // A reads rows >= rho(kP) - 1 while step k's DMA fills rows up to F(k)
+      const long need = F(k) - (rho(k * P) - 1) + 1;
+      if (need > nra) nra = need;
+    }
+    const long blo = k * P - lag - P;
+    if (blo + P + 32 > 0 && blo < total) {  // B reads rows >= rho(blo) - sB while A writes up to rho(kP + 31)
+      long wmax = k * P + 31;
+      if (wmax > total - 1) wmax = total - 1;
+      const long rlo = rho(blo > 0 ? blo : 0) - sB;
+      const long need = rho(wmax) - rlo + 1;
+      if (need > nrb) nrb = need;
+    }
+  }
+  // rows entering the A-in ring per step must fit the NPS pieces
+  for (long k = 0; k < ns; ++k)
+    if ((F(k) - F(k - 1)) * pp.ppr > 16) return pp;
+  if (F(-1) < 0) return pp;
+  pp.NRA = (int)(nra > 2 ? nra : 2);
+  pp.NRB = (int)(nrb > 2 ? nrb : 2);
+  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + 256 + 1024 <= g16p_lds_bytes();
+  return pp;
+}
+
 template <int NT, int SP>
 static int launch_block16w(const Block16WArgs& a, hipStream_t st) {
   int grid = cu_count();
@@ -876,6 +948,8 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
     return fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
                 "(use precision f32)", L.W);
   int rc;
+  const char* kenv = getenv("HONK_RES_KERNEL");
+  const bool pairs_ok = L.NT == 3 && SP == 2 && !(kenv && (kenv[0] == 'w' || kenv[0] == 'r'));
   if (use_w_kernel(L, d, SP)) {
     // weight-stationary kernel: tiles = (clip, dilation class, band of TH class rows), TH per dilation
     int nbc_last = 0;
@@ -884,8 +958,45 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       rc = (SP == 2) ? launch_conv0<__bf16, true, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
                      : launch_conv0<__bf16, false, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
       if (rc) return rc;
+      int grid = cu_count();
+      if (grid > n) grid = (int)n;
+      const int cpw = (int)cdiv(n, grid);
       for (int i = 1; i <= L.L; ++i) {
         const bool even = (i % 2) == 0;
+        // fused pair (i, i + 1): odd i, i + 1 not the last layer, dilation d or 2d
+        if (pairs_ok && !even && i + 1 < L.L) {
+          const int dA = dil_of(d, i), dB = dil_of(d, i + 1);
+          const int sB = dB == dA ? 1 : (dB == 2 * dA ? 2 : 0);
+          const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
+          const PairPlan pp = sB ? plan_pair(L, SP, dA, sB, cpw) : PairPlan{false, 0, 0, 0, 0, 0};
+          if (pp.ok && cb < 0xE0000000ull && (pp.ppr == 8 || pp.ppr == 4 || pp.ppr == 3)) {
+            Block16PArgs pa;
+            pa.R = R;
+            pa.wA = (const char*)(packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats);
+            pa.wB = (const char*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats);
+            pa.chunk_bytes = (unsigned)cb;
+            pa.nclips = (int)n;
+            pa.H = L.H;
+            pa.W = L.W;
+            pa.d = dA;
+            pa.lgd = 0;
+            while ((1 << pa.lgd) < dA) ++pa.lgd;
+            pa.sB = sB;
+            pa.lag = pp.lag;
+            pa.NRA = pp.NRA;
+            pa.NRB = pp.NRB;
+            pa.slotb = pp.slotb;
+            pa.ppr = pp.ppr;
+            TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
+            if (pp.ppr == 8) hipLaunchKernelGGL((block16p_kernel<3, 2, 8>), dim3(grid), dim3(256), 0, st, pa);
+            else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 2, 4>), dim3(grid), dim3(256), 0, st, pa);
+            else hipLaunchKernelGGL((block16p_kernel<3, 2, 3>), dim3(grid), dim3(256), 0, st, pa);
+            HONK_LAUNCH_CHECK("res block16p_kernel");
+            tl.done(st);
+            ++i;  // layer i + 1 done too
+            continue;
+          }
+        }
         Block16WArgs a;
         a.in = even ? X : R;
         a.res = even ? R : nullptr;

@@ -1,10 +1,14 @@
-"""Both bf16 / bf16x3 res block kernels on every shape, whichever the default
+"""Every bf16 / bf16x3 res block kernel on every shape, whichever the default
 dispatch picks: the row-band kernel (block16r_kernel, weights in LDS, border
-bias table) and the weight-stationary kernel (block16w_kernel, weights in the
-register file, folded-BN bias in the zero-padding channel C), forced with
-HONK_RES_KERNEL.  bf16x3: the fp32 parity bar (1e-4 absolute) vs the float64
-oracle and the reference's golden logits; bf16: the top-1 bar of test_gpu_bf16.
-The two kernels must also agree with each other."""
+bias table), the weight-stationary kernel (block16w_kernel, weights in the
+register file, folded-BN bias in the zero-padding channel C) and the fused
+layer-pair kernel (block16p_kernel: an odd layer and the even one after it in
+one launch, the odd layer's output kept in an LDS ring), forced with
+HONK_RES_KERNEL (p = pairs + weight-stationary, the bf16x3 default; w; r).
+bf16x3: the fp32 parity bar (1e-4 absolute) vs the float64 oracle and the
+reference's golden logits; bf16: the top-1 bar of test_gpu_bf16.  The kernels
+must also agree with each other (the pair kernel bit-for-bit with the
+weight-stationary one: same products, same order, same roundings)."""
 import numpy as np
 import pytest
 import torch
@@ -16,7 +20,7 @@ from golden_util import fixture_names, load_fixture, ref_configs
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-KERNELS = ("w", "r")
+KERNELS = ("p", "w", "r")
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -93,6 +97,28 @@ def test_bf16_shapes_kernels_agree(monkeypatch, name, override):
         assert np.abs(outs[k] - ref).max() <= 0.05
         assert np.mean(outs[k].argmax(1) == ref.argmax(1)) >= 0.9
     assert np.abs(outs["w"] - outs["r"]).max() <= 0.05
+
+
+# multi-clip streams per workgroup (batches above the CU count), pooled widths,
+# the mixed-dilation pairs (d, 2d) of res15, undilated res15, 33 maps
+PAIR_CASES = [("res15", {}, 600), ("res15", dict(n_feature_maps=33), 300), ("res26", {}, 520),
+              ("res8", {}, 700), ("res15", dict(use_dilation=False, n_layers=5), 260),
+              ("res15", dict(n_layers=7), 5)]
+
+
+@pytest.mark.parametrize("name,override,B", PAIR_CASES)
+def test_pair_kernel_bitwise_vs_w(monkeypatch, name, override, B):
+    cfg = dict(ref_configs()[name])
+    cfg.update(override)
+    params, x = _case(cfg, B, seed=31)
+    m = _module(cfg, params, name, "bf16x3")
+    monkeypatch.setenv("HONK_RES_KERNEL", "p")
+    outp = _run(m, x)
+    monkeypatch.setenv("HONK_RES_KERNEL", "w")
+    outw = _run(m, x)
+    assert np.array_equal(outp, outw), float(np.abs(outp - outw).max())
+    idx = list(range(0, B, max(1, B // 8)))[:8]
+    np.testing.assert_allclose(outp[idx], orc.forward(params, cfg, x[idx]), atol=1e-4, rtol=0)
 
 
 def test_w_kernel_batch_invariance(monkeypatch):
