@@ -8,11 +8,13 @@ NEVER = "a.H == 12345"  # a runtime-false condition the compiler cannot fold
 
 EPI = ("        if constexpr ((KE + E < KSA ? KE + E : KSA - 1) == S) epi_step(rolec, ec);",
        f"        if constexpr ((KE + E < KSA ? KE + E : KSA - 1) == S) if ({NEVER}) epi_step(rolec, ec);")
-RES = ("      if constexpr (ISB && S == 0) res_loads(po);", f"      if constexpr (ISB && S == 0) if ({NEVER}) res_loads(po);")
-DMA = ("        issue_piece(row, p - rr * a.ppr, row <= fcur);", f"        if ({NEVER}) issue_piece(row, p - rr * a.ppr, row <= fcur);")
-BAR = ("    __builtin_amdgcn_s_barrier();\n  };", "    if (" + NEVER + ") __builtin_amdgcn_s_barrier();\n  };")
-GEO = [("        const MG nxt = geo(qb + 32, ring, nr, sr, sc);", "        const MG nxt = cur;"),
-       ("        const MG nxt = geo(qb + P, ring, nr, sr, sc);", "        const MG nxt = cur;")]
+RES = ("      if constexpr (ISB && S == 0) res_loads(cur.pix);", f"      if constexpr (ISB && S == 0) if ({NEVER}) res_loads(cur.pix);")
+DMA = ("        dma(widx ? roff[rb] : roff[ra], widx ? rslot[rb] : rslot[ra], widx ? pb : pa, rr < nnew);",
+       f"        if ({NEVER}) dma(widx ? roff[rb] : roff[ra], widx ? rslot[rb] : rslot[ra], widx ? pb : pa, rr < nnew);")
+BAR = ("      __builtin_amdgcn_s_barrier();\n      // the first m-tile", "      if (" + NEVER + ") __builtin_amdgcn_s_barrier();\n      // the first m-tile")
+GEO = [("      if constexpr (S == KW) walk_adv(wk);", "      if constexpr (S == KW) if (" + NEVER + ") walk_adv(wk);"),
+       ("      if constexpr (S == KG) nxt = geo(wk);", "      if constexpr (S == KG) nxt = cur;")]
+BCAST = [("    return base + (int)(e & 0x7fu);\n  };", "    return zoff + (base & 0) + (int)(e & 0x7fu);\n  };")]
 PATCHES = {
     "base": [],
     "nobar": [BAR],
@@ -20,6 +22,7 @@ PATCHES = {
     "noepi": [EPI, RES],
     "nogeo": GEO,
     "mfma": [DMA, EPI, RES, BAR],
+    "bcast": BCAST,
 }
 
 def build(name):

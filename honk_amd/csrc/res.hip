@@ -765,14 +765,16 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
 struct PairPlan {
   bool ok;
-  int lag, NRA, NRB, slotb, ppr;
+  int lag, NRA, NRB, slotb, ppr, ppw;  // ppw: DMA pieces per A wave per step
 };
 static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw) {
-  PairPlan pp{false, 0, 0, 0, 0, 0};
+  PairPlan pp{false, 0, 0, 0, 0, 0, 0};
   const int P = 64, W = L.W, H = L.H;
-  const long CB = 32L * L.NT * SP;
-  pp.ppr = (int)((W * CB + 1023) / 1024);
-  pp.slotb = pp.ppr * 1024;
+  const long PXB = g16p_pxb(L.NT, SP);  // LDS pixel pitch
+  pp.ppr = (int)((W * PXB + 1023) / 1024);
+  // slot pitch: room for the DMA's whole pieces, = W * PXB mod 256 so that
+  // stream pixels stay at a constant LDS pitch across a row change
+  pp.slotb = (int)(W * PXB + ((pp.ppr * 1024 - W * PXB + 255) / 256) * 256);
   const long total = (long)cpw * H * W, rows_total = (long)cpw * H;
   if (total >= (1L << 24) || sB < 1 || sB > 2) return pp;
   auto rho = [&](long q) { return q / W; };
@@ -821,9 +823,11 @@ static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw) {
       if (need > nrb) nrb = need;
     }
   }
-  // rows entering the A-in ring per step must fit the NPS pieces
+  // rows entering the A-in ring per step: pieces per A wave
+  long maxrows = 0;
   for (long k = 0; k < ns; ++k)
-    if ((F(k) - F(k - 1)) * pp.ppr > 16) return pp;
+    if (F(k) - F(k - 1) > maxrows) maxrows = F(k) - F(k - 1);
+  pp.ppw = (int)((maxrows * pp.ppr + 1) / 2);
   if (F(-1) < 0) return pp;
   pp.NRA = (int)(nra > 2 ? nra : 2);
   pp.NRB = (int)(nrb > 2 ? nrb : 2);
@@ -969,7 +973,9 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
           const int sB = dB == dA ? 1 : (dB == 2 * dA ? 2 : 0);
           const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
           const PairPlan pp = sB ? plan_pair(L, SP, dA, sB, cpw) : PairPlan{false, 0, 0, 0, 0, 0};
-          if (pp.ok && cb < 0xE0000000ull && (pp.ppr == 8 || pp.ppr == 4 || pp.ppr == 3)) {
+          // instantiated pitches: W = 40 (res15), 20 (res26, 2x2 pool), 13 (res8, 4x3 pool)
+          const bool inst = (pp.ppr == 9 && pp.ppw <= 9) || (pp.ppr == 5 && pp.ppw <= 10) || (pp.ppr == 3 && pp.ppw <= 9);
+          if (pp.ok && cb < 0xE0000000ull && inst) {
             Block16PArgs pa;
             pa.R = R;
             pa.wA = (const char*)(packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats);
@@ -988,9 +994,9 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.slotb = pp.slotb;
             pa.ppr = pp.ppr;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
-            if (pp.ppr == 8) hipLaunchKernelGGL((block16p_kernel<3, 2, 8>), dim3(grid), dim3(256), 0, st, pa);
-            else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 2, 4>), dim3(grid), dim3(256), 0, st, pa);
-            else hipLaunchKernelGGL((block16p_kernel<3, 2, 3>), dim3(grid), dim3(256), 0, st, pa);
+            if (pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9>), dim3(grid), dim3(256), 0, st, pa);
+            else if (pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10>), dim3(grid), dim3(256), 0, st, pa);
+            else hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9>), dim3(grid), dim3(256), 0, st, pa);
             HONK_LAUNCH_CHECK("res block16p_kernel");
             tl.done(st);
             ++i;  // layer i + 1 done too
