@@ -243,44 +243,62 @@ def _res_geometry(cfg):
     return 101 // ph, 40 // pw, int(cfg["n_layers"]), 16 * ((C + 15) // 16)
 
 
-def res_roofline(prec, cfg, kms, nl, kfl, B, model):
-    """Roofline of the dominant res kernel (the dilated 3x3 block conv) for a precision mode.
+def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
+    """Roofline of the res block convs (the dilated 3x3 layers) for a precision mode.
 
-    MFMA-bound: achieved = ALGORITHMIC flop per launch (2 x 9 x C^2 x
-    H x W per clip-layer x clips per launch, no padding, one product per MAC) / the
-    mean launch time (HIP events on the launch stream); peak = the MFMA peak of the
-    mode in algorithmic flop (fp32 157.3 TF; bf16x3 = bf16 2.5 PF / 3 products;
-    bf16 2.5 PF).  Beside it: the kernel's algorithmic activation bytes as an HBM
-    rate, and the PMC-measured HBM traffic per launch."""
-    avg_s = (kms / max(nl, 1)) * 1e-3
-    clips = min(B, 4096)
-    fl = kfl / max(nl, 1)
-    ach = fl / avg_s / 1e12 if nl else None
-    peak = MODE_PEAK[prec]
+    MFMA-bound: achieved = ALGORITHMIC flop (2 x 9 x C^2 x H x W per
+    clip-layer, no padding, one product per MAC) over all timed block-kernel
+    launches / their summed time (HIP events on the launch stream); peak = the MFMA
+    peak of the mode in algorithmic flop (fp32 157.3 TF; bf16x3 = bf16 2.5 PF / 3
+    products; bf16 2.5 PF).  `plan` = the launches of one chunk's forward
+    (honk_res_launch_plan): block16p_kernel launches run a fused odd/even layer pair.
+    Beside it: the activation bytes the schedule moves per clip (a fused pair reads
+    its input once and the residual once and writes once; a single layer reads its
+    input [and the residual] and writes its output unless it is the last) as an
+    HBM rate, and the dominant kernel's PMC-measured HBM traffic per launch."""
     H, W, L, CP = _res_geometry(cfg)
+    ach = kfl / (kms * 1e-3) / 1e12 if nl and kms else None
+    peak = MODE_PEAK[prec]
+    clips = min(B, 4096)
+    chunk_fwds = nl / max(len(plan), 1)
     if prec == "f32":
-        fam, kname = "block_kernel", "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)"
-        traffic = load_traffic("block_kernel", clips, model)
         act = H * W * CP * 4
+        per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1))
+        dom, traffic = "block_kernel", load_traffic("block_kernel", clips, model)
+        kname = "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)"
     else:
         sp = 2 if prec == "bf16x3" else 1
-        fam = "block16r_kernel"
-        kname = f"honk::res::{fam}<..., SP={sp}> (dilated 3x3 conv, bf16 MFMA{', 3 products' if sp == 2 else ''})"
-        traffic = load_traffic(f"{fam}_sp{sp}", clips, model)
         act = H * W * CP * 2 * sp
-    # per clip-layer activation bytes the layer-by-layer schedule moves (read X [+R], write Y)
-    per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1)) / L
-    bw = per_clip * clips / avg_s / 1e9 if nl else None
+        per_clip, layer = 0, 1
+        for k in plan:
+            if k == "block16p_kernel":
+                per_clip += 3 * act
+                layer += 2
+            else:
+                per_clip += act * (1 + (1 if layer % 2 == 0 else 0) + (1 if layer < L else 0))
+                layer += 1
+        dom = max(set(plan), key=plan.count)
+        traffic = load_traffic(f"{dom}_sp{sp}", clips, model)
+        what = {"block16p_kernel": "fused odd + even layer pair", "block16w_kernel": "weight-stationary layer",
+                "block16r_kernel": "row-band layer"}
+        kname = (" + ".join(f"honk::res::{k}<..., SP={sp}> x{plan.count(k)} ({what[k]})"
+                            for k in sorted(set(plan), key=plan.index))
+                 + f" per chunk: dilated 3x3 convs, bf16 MFMA{', 3 products' if sp == 2 else ''}")
+    secs = kms * 1e-3
+    bw = per_clip * clips * chunk_fwds / secs / 1e9 if nl and secs else None
     out = {"bound": "mfma", "kernel": kname,
            "achieved": round(ach, 2) if ach else None, "peak": round(peak, 1), "unit": "TFLOP/s",
            "frac": round(ach / peak, 4) if ach else None,
-           "traffic": traffic,
-           "launches": nl, "avg_launch_ms": round(kms / max(nl, 1), 4), "clips_per_launch": clips,
-           "flop_per_launch": fl,
+           "traffic": traffic, "traffic_kernel": dom,
+           "launches": nl, "launch_plan_per_chunk": plan, "clips_per_chunk": clips,
+           "avg_ms_per_layer": round(kms / max(chunk_fwds * L, 1), 4),
+           "avg_ms_per_launch": {k: None for k in ()},
+           "flop_per_layer": kfl / max(chunk_fwds * L, 1),
            "flop_def": "algorithmic: 2*9*C^2*H*W per clip-layer (SURVEY §8(d)), no channel/tile padding",
-           "hbm": {"activation_bytes_per_launch": per_clip * clips,
+           "hbm": {"activation_bytes_per_clip": per_clip,
                    "achieved_GBs": round(bw, 1) if bw else None, "peak_GBs": HBM_PEAK_GBS,
                    "frac": round(bw / HBM_PEAK_GBS, 4) if bw else None}}
+    del out["avg_ms_per_launch"]
     if prec == "bf16x3" and ach:
         out["frac_of_raw_bf16_peak"] = round(ach / BF16_MFMA_PEAK_TFLOPS, 4)
     return out
@@ -346,11 +364,12 @@ def measure_res(ctx, args, name, prec, B, x=None, model=None):
     keep = getattr(model, "honk_precision", "f32")
     model.honk_precision = prec
     el, per, out, (kms, nl, kfl) = ctx.timed(model, x, args.steps, max(1, args.warmup))
+    plan = ctx.native.res_launch_plan(model._desc(101, 40), B)
     model.honk_precision = keep
     return {"value": round(ctx.world * B * args.steps / el, 1), "unit": "clips/s", "dtype": prec,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "per_rank_clips_s": [round(B * args.steps / t, 1) for t in per],
-            "roofline": res_roofline(prec, cfg, kms, nl, kfl, B, name),
+            "roofline": res_roofline(prec, cfg, kms, nl, kfl, B, name, plan),
             "parity": _sample_parity(model, cfg, x, out, orc, B),
             "note": PREC_NOTES[prec]}
 
@@ -551,7 +570,8 @@ def rank_main(args):
     value = world * B * args.steps / el
     flop_clip = orc.flops_per_clip(cfg)
     if is_res:
-        roof = res_roofline(prec, cfg, kms, nlaunch, kflop, B, args.model)
+        roof = res_roofline(prec, cfg, kms, nlaunch, kflop, B, args.model,
+                            ctx.native.res_launch_plan(model._desc(101, 40), B))
     else:
         avg_ms = kms / max(nlaunch, 1)
         ach = (kflop / max(nlaunch, 1)) / (avg_ms * 1e-3) / 1e12 if nlaunch else None

@@ -9,8 +9,7 @@ NEVER = "a.H == 12345"  # a runtime-false condition the compiler cannot fold
 EPI = ("        if constexpr ((KE + E < KSA ? KE + E : KSA - 1) == S) epi_step(rolec, ec);",
        f"        if constexpr ((KE + E < KSA ? KE + E : KSA - 1) == S) if ({NEVER}) epi_step(rolec, ec);")
 RES = ("      if constexpr (ISB && S == 0) res_loads(cur.pix);", f"      if constexpr (ISB && S == 0) if ({NEVER}) res_loads(cur.pix);")
-DMA = ("        dma(widx ? roff[rb] : roff[ra], widx ? rslot[rb] : rslot[ra], widx ? pb : pa, rr < nnew);",
-       f"        if ({NEVER}) dma(widx ? roff[rb] : roff[ra], widx ? rslot[rb] : rslot[ra], widx ? pb : pa, rr < nnew);")
+DMA = ("        dma(widx ? roff[rb] : roff[ra],", f"        if ({NEVER}) dma(widx ? roff[rb] : roff[ra],")
 BAR = ("      __builtin_amdgcn_s_barrier();\n      // the first m-tile", "      if (" + NEVER + ") __builtin_amdgcn_s_barrier();\n      // the first m-tile")
 GEO = [("      if constexpr (S == KW) walk_adv(wk);", "      if constexpr (S == KW) if (" + NEVER + ") walk_adv(wk);"),
        ("      if constexpr (S == KG) nxt = geo(wk);", "      if constexpr (S == KG) nxt = cur;")]
@@ -23,6 +22,11 @@ PATCHES = {
     "nogeo": GEO,
     "mfma": [DMA, EPI, RES, BAR],
     "bcast": BCAST,
+    "nosb": [("      __builtin_amdgcn_sched_barrier(0);\n      const u32x4 (&ac)[SP]", "      const u32x4 (&ac)[SP]")],
+    "aonly": [("        if (it == 0) run_mtile(rolec,", "        if (ISB && a.H != 12345) { for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f}; } else if (it == 0) run_mtile(rolec,"),
+              ("        else run_mtile(rolec, std::integral_constant<bool, false>{}", "        else if (!(ISB && a.H != 12345)) run_mtile(rolec, std::integral_constant<bool, false>{}")],
+    "bonly": [("        if (it == 0) run_mtile(rolec,", "        if (!ISB && a.H != 12345) { for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f}; } else if (it == 0) run_mtile(rolec,"),
+              ("        else run_mtile(rolec, std::integral_constant<bool, false>{}", "        else if (!(!ISB && a.H != 12345)) run_mtile(rolec, std::integral_constant<bool, false>{}")],
 }
 
 def build(name):

@@ -38,6 +38,8 @@ class CnnDesc(ctypes.Structure):
 _PROTOS = {
     "honk_res_packed_floats": (ctypes.c_size_t, [ctypes.POINTER(ResDesc)]),
     "honk_res_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(ResDesc), ctypes.c_int64]),
+    "honk_res_launch_plan": (ctypes.c_int, [ctypes.POINTER(ResDesc), ctypes.c_int64, ctypes.c_int32,
+                                            ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     "honk_res_pack": (ctypes.c_int, [ctypes.POINTER(ResDesc), ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32,
                                      c_f32p, ctypes.c_void_p]),
     "honk_res_forward": (ctypes.c_int, [ctypes.POINTER(ResDesc), c_f32p, c_f32p, c_f32p, ctypes.c_int64,
@@ -140,3 +142,18 @@ def timing_read():
     fl = ctypes.c_double()
     check(load().honk_timing_read(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)), "honk_timing_read")
     return ms.value, n.value, fl.value
+
+
+# HONK_KERNEL_* of include/honk_hip.h
+KERNEL_NAMES = {1: "block_kernel", 2: "block16r_kernel", 3: "block16w_kernel", 4: "block16p_kernel"}
+
+
+def res_launch_plan(desc, batch: int, n_cus: int = 0):
+    """The block-layer launches honk_res_forward makes per batch chunk, as kernel
+    names (HONK_KERNEL_* codes mapped through KERNEL_NAMES).  Host-only."""
+    lib = load()
+    kinds = (ctypes.c_int32 * 256)()
+    n = lib.honk_res_launch_plan(ctypes.byref(desc), int(batch), int(n_cus), kinds, 256)
+    if n < 0:
+        check(-n, "honk_res_launch_plan")
+    return [KERNEL_NAMES[kinds[i]] for i in range(min(n, 256))]

@@ -835,6 +835,25 @@ static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw) {
   return pp;
 }
 
+// The fused pair for layers (i, i + 1) of a chunk of n clips on `grid`
+// workgroups, or ok = false: i odd, i + 1 not the last layer (the pair kernel has
+// no channel-sum epilogue), B's dilation d or 2d of A's, 45-map class bf16x3 on the
+// weight-stationary path, an instantiated row pitch, a plan that fits the LDS.
+static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t n, int grid, int i) {
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0};
+  const char* kenv = getenv("HONK_RES_KERNEL");
+  if (L.NT != 3 || SP != 2 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
+  if (i % 2 == 0 || i + 1 >= L.L) return no;
+  const int dA = dil_of(d, i), dB = dil_of(d, i + 1);
+  const int sB = dB == dA ? 1 : (dB == 2 * dA ? 2 : 0);
+  const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
+  if (!sB || cb >= 0xE0000000ull) return no;
+  const PairPlan pp = plan_pair(L, SP, dA, sB, (int)cdiv(n, grid));
+  // instantiated pitches: W = 40 (res15), 20 (res26, 2x2 pool), 13 (res8, 4x3 pool)
+  const bool inst = (pp.ppr == 9 && pp.ppw <= 9) || (pp.ppr == 5 && pp.ppw <= 10) || (pp.ppr == 3 && pp.ppw <= 9);
+  return pp.ok && inst ? pp : no;
+}
+
 template <int NT, int SP>
 static int launch_block16w(const Block16WArgs& a, hipStream_t st) {
   int grid = cu_count();
@@ -952,8 +971,6 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
     return fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
                 "(use precision f32)", L.W);
   int rc;
-  const char* kenv = getenv("HONK_RES_KERNEL");
-  const bool pairs_ok = L.NT == 3 && SP == 2 && !(kenv && (kenv[0] == 'w' || kenv[0] == 'r'));
   if (use_w_kernel(L, d, SP)) {
     // weight-stationary kernel: tiles = (clip, dilation class, band of TH class rows), TH per dilation
     int nbc_last = 0;
@@ -964,18 +981,13 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       if (rc) return rc;
       int grid = cu_count();
       if (grid > n) grid = (int)n;
-      const int cpw = (int)cdiv(n, grid);
       for (int i = 1; i <= L.L; ++i) {
         const bool even = (i % 2) == 0;
-        // fused pair (i, i + 1): odd i, i + 1 not the last layer, dilation d or 2d
-        if (pairs_ok && !even && i + 1 < L.L) {
-          const int dA = dil_of(d, i), dB = dil_of(d, i + 1);
-          const int sB = dB == dA ? 1 : (dB == 2 * dA ? 2 : 0);
-          const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
-          const PairPlan pp = sB ? plan_pair(L, SP, dA, sB, cpw) : PairPlan{false, 0, 0, 0, 0, 0};
-          // instantiated pitches: W = 40 (res15), 20 (res26, 2x2 pool), 13 (res8, 4x3 pool)
-          const bool inst = (pp.ppr == 9 && pp.ppw <= 9) || (pp.ppr == 5 && pp.ppw <= 10) || (pp.ppr == 3 && pp.ppw <= 9);
-          if (pp.ok && cb < 0xE0000000ull && inst) {
+        {
+          const PairPlan pp = pair_at(L, d, SP, n, grid, i);
+          if (pp.ok) {
+            const int dA = dil_of(d, i);
+            const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
             Block16PArgs pa;
             pa.R = R;
             pa.wA = (const char*)(packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats);
@@ -987,7 +999,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.d = dA;
             pa.lgd = 0;
             while ((1 << pa.lgd) < dA) ++pa.lgd;
-            pa.sB = sB;
+            pa.sB = dil_of(d, i + 1) == dA ? 1 : 2;
             pa.lag = pp.lag;
             pa.NRA = pp.NRA;
             pa.NRB = pp.NRB;
@@ -1094,6 +1106,40 @@ size_t honk_res_packed_floats(const honk_res_desc* d) {
   Layout L;
   if (make_layout(d, &L) != HONK_OK) return 0;
   return L.total;
+}
+
+int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, int32_t* kinds, int32_t max_kinds) {
+  Layout L;
+  int rc = make_layout(d, &L);
+  if (rc) return -rc;
+  if (batch < 1) return -fail(HONK_ERR_ARG, "batch < 1");
+  const int64_t n = chunk_clips(L, batch);
+  int grid = n_cus > 0 ? n_cus : cu_count();
+  if (grid > n) grid = (int)n;
+  int cnt = 0;
+  auto put = [&](int k) {
+    if (kinds && cnt < max_kinds) kinds[cnt] = k;
+    ++cnt;
+  };
+  if (L.prec == HONK_PREC_F32) {
+    for (int i = 1; i <= L.L; ++i) put(HONK_KERNEL_BLOCK_F32);
+    return cnt;
+  }
+  const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;
+  if (plan_block16r(L, SP).TH == 0) return -fail(HONK_ERR_UNSUPPORTED, "width beyond the row-band staging plan");
+  if (!use_w_kernel(L, d, SP)) {
+    for (int i = 1; i <= L.L; ++i) put(HONK_KERNEL_ROWBAND);
+    return cnt;
+  }
+  for (int i = 1; i <= L.L; ++i) {
+    if (pair_at(L, d, SP, n, grid, i).ok) {
+      put(HONK_KERNEL_PAIR);
+      ++i;
+    } else {
+      put(HONK_KERNEL_WSTAT);
+    }
+  }
+  return cnt;
 }
 
 size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {

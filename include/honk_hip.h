@@ -70,6 +70,17 @@ size_t honk_res_packed_floats(const honk_res_desc* d);
 /* bytes of scratch needed by honk_res_forward for `batch` clips */
 size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch);
 /*
+ * The block-layer launches honk_res_forward makes per batch chunk, in order: kinds[i]
+ * = HONK_KERNEL_* (up to max_kinds written).  Returns the launch count, or minus a
+ * status code.  n_cus = 0: the current device's CU count (the pair kernel's plan
+ * depends on clips per workgroup).  Host-only; no GPU work.
+ */
+#define HONK_KERNEL_BLOCK_F32 1 /* fp32-MFMA layer (block_kernel)                        */
+#define HONK_KERNEL_ROWBAND 2   /* bf16 / bf16x3 row-band layer (block16r_kernel)          */
+#define HONK_KERNEL_WSTAT 3     /* bf16 / bf16x3 weight-stationary layer (block16w_kernel) */
+#define HONK_KERNEL_PAIR 4      /* fused odd + even layer pair (block16p_kernel)           */
+int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, int32_t* kinds, int32_t max_kinds);
+/*
  * Pack a state_dict into kernel layout.  tensors[] (device, fp32, contiguous),
  * in this order (n_tensors = 3*n_layers + 3):
  *   conv0.weight [C,1,3,3], conv1.weight .. conv{L}.weight [C,C,3,3],

@@ -219,3 +219,35 @@ def test_legacy_checkpoint_without_num_batches_tracked(tmp_path):
     torch.save(bad, fn)
     with pytest.raises(RuntimeError):
         hm.find_model("res15")(cfg).load(fn)
+
+
+def test_res_launch_plan_host_only(monkeypatch):
+    """honk_res_launch_plan (host-only): which block kernels a forward launches per
+    chunk -- res15 bf16x3: six fused odd/even pairs then the last layer on the
+    weight-stationary kernel; res26 likewise (last pair unfused: the pair kernel has
+    no channel-sum epilogue); HONK_RES_KERNEL=w / r force single layers; f32 and
+    19-map bf16x3 keep their kernels."""
+    from honk_amd import _native
+    from honk_amd import model as hm
+    lib = _native.load()
+    del lib
+
+    def plan(name, prec, batch=4096, **ov):
+        cfg = dict(hm.find_config(name))
+        cfg.update(ov)
+        m = hm.find_model(name)(cfg)
+        m.honk_precision = prec
+        return _native.res_launch_plan(m._desc(101, 40), batch, n_cus=256)
+
+    monkeypatch.delenv("HONK_RES_KERNEL", raising=False)
+    assert plan("res15", "bf16x3") == ["block16p_kernel"] * 6 + ["block16w_kernel"]
+    assert plan("res15", "bf16x3", batch=3) == ["block16p_kernel"] * 6 + ["block16w_kernel"]
+    assert plan("res26", "bf16x3") == ["block16p_kernel"] * 11 + ["block16w_kernel"] * 2
+    assert plan("res8", "bf16x3") == ["block16p_kernel"] * 2 + ["block16w_kernel"] * 2
+    assert plan("res15", "f32") == ["block_kernel"] * 13
+    assert plan("res15", "bf16") == ["block16r_kernel"] * 13
+    assert plan("res15-narrow", "bf16x3") == ["block16r_kernel"] * 13
+    monkeypatch.setenv("HONK_RES_KERNEL", "w")
+    assert plan("res15", "bf16x3") == ["block16w_kernel"] * 13
+    monkeypatch.setenv("HONK_RES_KERNEL", "r")
+    assert plan("res15", "bf16x3") == ["block16r_kernel"] * 13

@@ -58,6 +58,9 @@ def main():
         for fam in ("block16r_kernel",):  # split by SP (3rd template argument): sp1 = bf16, sp2 = bf16x3
             if f"::{fam}<" in k:
                 return f"{fam}_sp" + k.split("<")[1].split(",")[2].strip()
+        for fam in ("block16w_kernel", "block16p_kernel"):  # SP is the 2nd template argument
+            if f"::{fam}<" in k:
+                return f"{fam}_sp" + k.split("<")[1].split(",")[1].strip()
         for fam in ("block_kernel", "conv_gemm_kernel"):
             if f"::{fam}<" in k:
                 return fam
