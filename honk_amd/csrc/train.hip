@@ -199,6 +199,108 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------- //
+// conv3x3m_kernel<C> (C <= 20): the same convolution (forward / input gradient) as
+// conv3x3_kernel on v_mfma_f32_16x16x4_f32, as an implicit GEMM D[o][p] = sum_k
+// W'[o][k] X[k][p] over k = 9 c + t (input channel c, tap t) -- the order of
+// conv3x3_kernel's FMA chain, and the MFMA is an fmaf chain over its 4 k: the two
+// kernels agree bit for bit.  (Training is ill-conditioned where train-mode
+// BatchNorm meets a nearly dead channel: a different summation order in one
+// layer moved res15-narrow's gradients by 1e-2 from float64.)  Lane (pixel p, kk)
+// reads X[4 s + kk][p] = plane c, tap t of the staged band: a per-lane offset per
+// k-step (16-bit, packed two per VGPR) plus the pixel's base.  The layer's weight
+// operand (ceil(9C / 4) k-steps x 2 out-tiles floats per lane) stays in VGPRs;
+// two workgroups per CU.  Output lane (p, g) holds channels 16 n + 4 g .. +3.
+// ---------------------------------------------------------------------------- //
+constexpr int TM_XL = 64 * 1024;  // staged tile bytes
+__host__ __device__ inline int tm_ps(int rows, int Wp) {  // plane stride (floats), = 16 mod 32
+  const int f = rows * Wp;
+  return f + ((16 - f % 32) + 32) % 32;
+}
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+template <int C>
+__global__ __launch_bounds__(256, 2) void conv3x3m_kernel(Conv3Args a) {
+  static_assert(C <= 20, "conv3x3m_kernel: C <= 20");
+  constexpr int K = 9 * C, KS = (K + 3) / 4;
+  __shared__ __attribute__((aligned(16))) float xl[TM_XL / 4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int d = a.g.d, Wp = a.W + 2 * d;
+  const int PS = tm_ps(a.g.TH + 2, Wp);  // every tile's planes at the longest band's stride
+  // the weight operand wr[s][n] = W'[16 n + i16][4 s + kk] and the lane's LDS offset
+  // of k = 4 s + kk (c PS + row / column shift of tap t; the K pad reads plane 0 x 0)
+  float wr[KS][2];
+  unsigned koff[(KS + 1) / 2];
+#pragma unroll
+  for (int s = 0; s < (KS + 1) / 2; ++s) koff[s] = 0;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + kk, c = k / 9, t = k - 9 * c;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int o = 16 * n + i16;
+      float v = 0.f;
+      if (o < C && k < K) v = a.flip ? a.w[(c * C + o) * 9 + 8 - t] : a.w[(o * C + c) * 9 + t];
+      wr[s][n] = v;
+    }
+    const unsigned off = k < K ? (unsigned)(c * PS + (t / 3) * Wp + (t % 3) * d) : 0u;
+    koff[s >> 1] |= off << (16 * (s & 1));
+  }
+  for (int tile = blockIdx.x; tile < a.B * a.g.nband; tile += gridDim.x) {
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, a.H, tile - b * a.g.nband, r, k0, th);
+    const int rows = th + 2, plane = rows * Wp;
+    __syncthreads();  // previous tile's readers done
+    const float* xb = a.x + (size_t)b * C * a.H * a.W;
+    for (int i = tid; i < C * plane; i += 256) {
+      const int c = i / plane, rc = i - c * plane, rr = rc / Wp, col = rc - rr * Wp;
+      const int h = r + (k0 - 1 + rr) * d, w = col - d;
+      xl[c * PS + rc] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
+    }
+    __syncthreads();
+    const int npx = th * a.W, nmt = (npx + 15) >> 4;
+    float* yb = a.y + (size_t)b * C * a.H * a.W;
+    for (int m = wave; m < nmt; m += 4) {
+      const int p = 16 * m + i16;
+      const bool pv = p < npx;
+      const int j = pv ? p / a.W : 0, col = pv ? p - j * a.W : 0;
+      const float* xp = xl + j * Wp + col;
+      f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float xv = xp[(koff[s >> 1] >> (16 * (s & 1))) & 0xffffu];
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s][0], xv, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s][1], xv, acc[1], 0, 0, 0);
+      }
+      if (pv) {
+        const size_t pix = (size_t)(r + (k0 + j) * d) * a.W + col;
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int o = 16 * n + 4 * kk + i;
+            if (o < C) yb[(size_t)o * a.H * a.W + pix] = acc[n][i];
+          }
+      }
+    }
+  }
+}
+
+// class rows per conv3x3m_kernel tile: C planes of (TH + 2) x (W + 2d) (+ pad) in TM_XL
+static int tm_rows(int C, int H, int W, int d) {
+  const int Wp = W + 2 * d;
+  int th = (TM_XL / 4 / C - 32) / Wp - 2;
+  const int hc = (H + d - 1) / d;
+  if (th > hc) th = hc;
+  if (th < 1 || (long)C * (th + 2) * Wp >= 65536) return 0;  // 16-bit k-step offsets
+  const int nb = (hc + th - 1) / th;
+  return (hc + nb - 1) / nb;
+}
+
 struct WgradArgs {
   const float* x;   // [B][C][H][W]
   const float* dy;  // [B][C][H][W]
@@ -520,7 +622,12 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
   const int np = (int)cdiv((int64_t)a.g.TH * w_, 256);  // output pixels per thread
-  if (c == 19) {
+  const char* ke = getenv("HONK_TRAIN_CONV");
+  if (c == 19 && !(ke && ke[0] == 'v') && train::tm_rows(c, h, w_, dil) > 0) {
+    a.g = train::class_bands(h, dil, train::tm_rows(c, h, w_, dil));
+    const int gm = (int)std::min<int64_t>((int64_t)a.B * a.g.nband, 2 * (int64_t)cu_count());
+    hipLaunchKernelGGL((train::conv3x3m_kernel<19>), dim3(gm), dim3(256), 0, st, a);
+  } else if (c == 19) {
     if (np <= 1) hipLaunchKernelGGL((train::conv3x3_kernel<19, 1>), dim3(grid), dim3(256), 0, st, a);
     else if (np == 2) hipLaunchKernelGGL((train::conv3x3_kernel<19, 2>), dim3(grid), dim3(256), 0, st, a);
     else if (np == 3) hipLaunchKernelGGL((train::conv3x3_kernel<19, 3>), dim3(grid), dim3(256), 0, st, a);

@@ -130,3 +130,20 @@ def test_native_train_minimum_batch_and_eval_switch():
         gpu = m(x).cpu()
         cpu = m.cpu()(x.cpu())
     torch.testing.assert_close(gpu, cpu, rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,H,W,d", [(3, 50, 20, 1), (2, 101, 40, 2), (3, 101, 40, 4), (2, 101, 40, 16), (2, 9, 5, 3)])
+def test_conv3x3_mfma_bitwise_vs_valu(monkeypatch, B, H, W, d):
+    """The 19-map training conv on fp32 MFMA (conv3x3m_kernel, the default) sums in the
+    VALU kernel's order (k = 9 c + t, an fmaf chain): forward and input gradient are
+    bit-identical to HONK_TRAIN_CONV=v (train-mode BatchNorm makes the step sensitive
+    to any change of rounding, so the order is part of the contract)."""
+    g = torch.Generator(device=DEV).manual_seed(7 + H + d)
+    x = torch.randn(B, 19, H, W, device=DEV, generator=g)
+    w = torch.randn(19, 19, 3, 3, device=DEV, generator=g) * 0.1
+    outs = {}
+    for k in ("m", "v"):
+        monkeypatch.setenv("HONK_TRAIN_CONV", k)
+        outs[k] = (hc._conv(x, w, flip=False, d=d), hc._conv(x, w, flip=True, d=d))
+    assert torch.equal(outs["m"][0], outs["v"][0])
+    assert torch.equal(outs["m"][1], outs["v"][1])
