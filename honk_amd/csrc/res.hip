@@ -355,13 +355,13 @@ __device__ __forceinline__ void store4(__bf16* o, f32x4 v) {
 // accesses by the pixel pitch).  The packed weights are zero for channels >= C.
 // ONES: channel C (< CP) holds 1.0 -- the bias channel of the weight-stationary
 // bf16 kernels (pack_block16_kernel)
-template <int PH, int PW, typename OT, bool SPLIT, bool ONES>
+template <int PH, int PW, typename OT, bool SPLIT, bool ONES, int CPM = 48>
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, OT* __restrict__ out,
                                                     const float* __restrict__ w0, int n, int Hin,
                                                     int Win, int H, int W, int C, int CP) {
   // SPLIT (bf16x3 activations): per pixel [hi CP][lo CP] bf16, lo = bf16(v - hi)
   constexpr int PPX = SPLIT ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) OT stage[256 * 48 * PPX];
+  __shared__ __attribute__((aligned(16))) OT stage[256 * CPM * PPX];  // CPM >= CP
   const int64_t p0 = (int64_t)blockIdx.x * 256;
   const int64_t gid = p0 + threadIdx.x;
   const int64_t total = (int64_t)n * H * W;
@@ -590,8 +590,9 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   if (d->n_maps < 1 || d->n_layers < 0 || d->n_labels < 1 || d->height < 1 || d->width < 1)
     return fail(HONK_ERR_ARG, "bad res descriptor (n_maps=%d n_layers=%d n_labels=%d h=%d w=%d)",
                 d->n_maps, d->n_layers, d->n_labels, d->height, d->width);
-  if (d->n_maps > 48)
-    return fail(HONK_ERR_UNSUPPORTED, "n_feature_maps=%d > 48 is not supported by the gfx950 kernels",
+  if (d->n_maps > 64 || (d->n_maps > 48 && d->precision != HONK_PREC_F32))
+    return fail(HONK_ERR_UNSUPPORTED,
+                "n_feature_maps=%d: the gfx950 kernels take up to 64 maps in precision f32, 48 in bf16 / bf16x3",
                 d->n_maps);
   L->C = d->n_maps;
   L->NT = (d->n_maps + 15) / 16;
@@ -650,6 +651,7 @@ static Plan plan_block(const Layout& L) {
   for (int mi = 0; mi < 5; ++mi) {
     const int MT = mts[mi];
     if (L.NT == 3 && MT > 5) continue;  // VGPR budget at 3 waves/SIMD
+    if (L.NT == 4 && MT != 2) continue;  // 16 waves (4 per SIMD): MT = 2 fits 128 VGPRs
     const int MP = 16 * MT * MW;
     const int thmax = MP / L.W;
     if (thmax < 1) continue;
@@ -928,6 +930,7 @@ static int dispatch_block(const Plan& p, const BlockArgs& a, hipStream_t st) {
   HONK_CASE(1, 2) HONK_CASE(1, 3) HONK_CASE(1, 4) HONK_CASE(1, 5) HONK_CASE(1, 6)
   HONK_CASE(2, 2) HONK_CASE(2, 3) HONK_CASE(2, 4) HONK_CASE(2, 5) HONK_CASE(2, 6)
   HONK_CASE(3, 2) HONK_CASE(3, 3) HONK_CASE(3, 4) HONK_CASE(3, 5)
+  HONK_CASE(4, 2)
 #undef HONK_CASE
   return fail(HONK_ERR_UNSUPPORTED, "no block kernel for NT=%d MT=%d", p.NT, p.MT);
 }
@@ -939,8 +942,12 @@ static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w
   const int blocks = (int)cdiv(total, 256);
 #define HONK_C0(PH, PW)                                                                               \
   if (L.ph == PH && L.pw == PW) {                                                                     \
-    hipLaunchKernelGGL((conv0_kernel<PH, PW, OT, SPLIT, ONES>), dim3(blocks), dim3(256), 0, st, x, out, w0, \
-                       (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                                    \
+    if (L.CP <= 48)                                                                                   \
+      hipLaunchKernelGGL((conv0_kernel<PH, PW, OT, SPLIT, ONES>), dim3(blocks), dim3(256), 0, st, x, out, w0, \
+                         (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                                  \
+    else                                                                                              \
+      hipLaunchKernelGGL((conv0_kernel<PH, PW, OT, SPLIT, ONES, 64>), dim3(blocks), dim3(256), 0, st, x, out, \
+                         w0, (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                              \
     HONK_LAUNCH_CHECK("res conv0_kernel");                                                            \
     return HONK_OK;                                                                                   \
   }

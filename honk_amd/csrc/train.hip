@@ -144,10 +144,18 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
     const int rows = th + 2, plane = rows * Wp;
     __syncthreads();  // previous tile's readers done (and the weights staged)
     const float* xb = a.x + (size_t)b * C * a.H * a.W;
-    for (int i = tid; i < C * plane; i += 256) {
-      const int c = i / plane, rc = i - c * plane, rr = rc / Wp, col = rc - rr * Wp;
-      const int h = r + (k0 - 1 + rr) * d, w = col - d;
-      xl[i] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
+    for (int i0 = tid; i0 < C * plane; i0 += 8 * 256) {  // 8 loads in flight per thread
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 256;
+        const int c = i / plane, rc = i - c * plane, rr = rc / Wp, col = rc - rr * Wp;
+        const int h = r + (k0 - 1 + rr) * d, w = col - d;
+        v[u] = (i < C * plane && h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + u * 256 < C * plane) xl[i0 + u * 256] = v[u];
     }
     __syncthreads();
     // packed fp32 FMA (v_pk_fma_f32): output channel pairs share the pixel's input
@@ -249,17 +257,43 @@ __global__ __launch_bounds__(256, 2) void conv3x3m_kernel(Conv3Args a) {
     const unsigned off = k < K ? (unsigned)(c * PS + (t / 3) * Wp + (t % 3) * d) : 0u;
     koff[s >> 1] |= off << (16 * (s & 1));
   }
+  // staging: thread = (row lane rl, column col) copies column col of staged rows
+  // rl, rl + SR, ...; the d halo columns of every row are zeroed once here and
+  // never written again (every tile stages the longest band's R rows)
+  const int R = a.g.TH + 2, SR = 256 / a.W, rl0 = tid / a.W, col0 = tid - rl0 * a.W;
+  for (int i = tid; i < C * R * 2 * d; i += 256) {
+    const int row = i / (2 * d), e = i - row * (2 * d);
+    const int c = row / R, rr = row - c * R;
+    xl[c * PS + rr * Wp + (e < d ? e : a.W + e)] = 0.f;
+  }
   for (int tile = blockIdx.x; tile < a.B * a.g.nband; tile += gridDim.x) {
     const int b = tile / a.g.nband;
     int r, k0, th;
     band_of(a.g, a.H, tile - b * a.g.nband, r, k0, th);
-    const int rows = th + 2, plane = rows * Wp;
     __syncthreads();  // previous tile's readers done
-    const float* xb = a.x + (size_t)b * C * a.H * a.W;
-    for (int i = tid; i < C * plane; i += 256) {
-      const int c = i / plane, rc = i - c * plane, rr = rc / Wp, col = rc - rr * Wp;
-      const int h = r + (k0 - 1 + rr) * d, w = col - d;
-      xl[c * PS + rc] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
+    if (rl0 < SR) {
+      // 8 loads in flight per thread (a serial load-store walk waits out the HBM
+      // latency on every row)
+      const float* xb = a.x + (size_t)b * C * a.H * a.W + col0;
+      const float invR = 1.0f / (float)R;
+      for (int row0 = rl0; row0 < C * R; row0 += 8 * SR) {
+        float v[8];
+        int dst[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int row = row0 + u * SR;
+          int c = (int)((float)row * invR);  // exact: row < 2^16 (host-checked C R < 65536)
+          c += (row - c * R >= R) ? 1 : ((row - c * R < 0) ? -1 : 0);
+          const int rr = row - c * R;
+          const int h = r + (k0 - 1 + rr) * d;
+          const bool ok = row < C * R && h >= 0 && h < a.H;
+          v[u] = ok ? xb[((size_t)c * a.H + h) * a.W] : 0.f;
+          dst[u] = row < C * R ? c * PS + rr * Wp + d + col0 : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (dst[u] >= 0) xl[dst[u]] = v[u];
+      }
     }
     __syncthreads();
     const int npx = th * a.W, nmt = (npx + 15) >> 4;
@@ -296,7 +330,7 @@ static int tm_rows(int C, int H, int W, int d) {
   int th = (TM_XL / 4 / C - 32) / Wp - 2;
   const int hc = (H + d - 1) / d;
   if (th > hc) th = hc;
-  if (th < 1 || (long)C * (th + 2) * Wp >= 65536) return 0;  // 16-bit k-step offsets
+  if (th < 1 || W > 256 || (long)C * (th + 2) * Wp >= 65536) return 0;  // 16-bit k-step offsets
   const int nb = (hc + th - 1) / th;
   return (hc + nb - 1) / nb;
 }
@@ -344,17 +378,37 @@ __global__ __launch_bounds__(512) void wgrad3x3_kernel(WgradArgs a) {
     band_of(a.g, a.H, tile - b * a.g.nband, r, k0, th);
     const int rows = th + 2, plane = rows * Wp, npx = th * a.W;
     __syncthreads();
+    // staging with 8 loads in flight per thread (a serial load-store loop waits out
+    // the HBM latency on every element)
     const float* xb = a.x + (size_t)b * C * a.H * a.W;
-    for (int i = tid; i < C * plane; i += 512) {
-      const int c = i / plane, rc = i - c * plane, rr = rc / Wp, col = rc - rr * Wp;
-      const int h = r + (k0 - 1 + rr) * d, w = col - d;
-      xl[i] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
+    for (int i0 = tid; i0 < C * plane; i0 += 8 * 512) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 512;
+        const int c = i / plane, rc = i - c * plane, rr = rc / Wp, col = rc - rr * Wp;
+        const int h = r + (k0 - 1 + rr) * d, w = col - d;
+        v[u] = (i < C * plane && h >= 0 && h < a.H && w >= 0 && w < a.W) ? xb[((size_t)c * a.H + h) * a.W + w] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + u * 512 < C * plane) xl[i0 + u * 512] = v[u];
     }
     const float* db = a.dy + (size_t)b * C * a.H * a.W;
-    for (int i = tid; i < CW * npx; i += 512) {  // dy transposed to [pixel][out]
-      const int o = i / npx, p = i - o * npx;
-      const int j = p / a.W, col = p - j * a.W;
-      dl[p * CW + o] = o < C ? db[(size_t)o * a.H * a.W + (size_t)(r + (k0 + j) * d) * a.W + col] : 0.f;
+    for (int i0 = tid; i0 < CW * npx; i0 += 8 * 512) {  // dy transposed to [pixel][out]
+      float v[8];
+      int dst[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 512;
+        const int o = i / npx, p = i - o * npx;
+        const int j = p / a.W, col = p - j * a.W;
+        v[u] = (i < CW * npx && o < C) ? db[(size_t)o * a.H * a.W + (size_t)(r + (k0 + j) * d) * a.W + col] : 0.f;
+        dst[u] = i < CW * npx ? p * CW + o : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (dst[u] >= 0) dl[dst[u]] = v[u];
     }
     __syncthreads();
     if (active) {

@@ -45,7 +45,7 @@ extern "C" {
 /* ---- SpeechResModel (res8/15/26[-narrow]); utils/model.py:82-121 ------------- */
 typedef struct honk_res_desc {
   int32_t n_labels;       /* config["n_labels"]                                  */
-  int32_t n_maps;         /* config["n_feature_maps"]   (1..48 supported)        */
+  int32_t n_maps;         /* config["n_feature_maps"] (1..64 in f32, 1..48 bf16*) */
   int32_t n_layers;       /* config["n_layers"]                                  */
   int32_t use_dilation;   /* config["use_dilation"]: conv{i} dilation 2**((i-1)//3) */
   int32_t pool_h, pool_w; /* config["res_pool"], or 0,0 when absent              */

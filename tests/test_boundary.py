@@ -187,10 +187,15 @@ def test_abi_queries_without_gpu():
                            height=101, width=67, precision=_native.PRECISIONS["bf16x3"])
     assert lib.honk_res_workspace_bytes(wide, 10) == 0
     assert b"row-band staging plan" in lib.honk_last_error()
-    bad = _native.ResDesc(n_labels=12, n_maps=64, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
+    bad = _native.ResDesc(n_labels=12, n_maps=65, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
                           height=101, width=40)
     assert lib.honk_res_packed_floats(bad) == 0
-    assert b"not supported" in lib.honk_last_error()
+    assert b"up to 64 maps" in lib.honk_last_error()
+    wide64 = _native.ResDesc(n_labels=12, n_maps=64, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
+                             height=101, width=40)  # f32 (precision 0): 64 maps take NT = 4
+    assert lib.honk_res_packed_floats(wide64) > 0
+    wide64.precision = _native.PRECISIONS["bf16x3"]
+    assert lib.honk_res_packed_floats(wide64) == 0
     assert b"gfx950" in lib.honk_version()
 
 

@@ -68,6 +68,7 @@ def test_res_vs_oracle(name, B):
 
 @pytest.mark.parametrize("override", [
     dict(n_feature_maps=16), dict(n_feature_maps=32), dict(n_feature_maps=48), dict(n_feature_maps=1),
+    dict(n_feature_maps=49), dict(n_feature_maps=64), dict(n_feature_maps=57, n_layers=5, use_dilation=True),
     dict(n_layers=0), dict(n_layers=1), dict(n_layers=2), dict(n_layers=3, use_dilation=True),
     dict(res_pool=(2, 3), n_layers=4), dict(res_pool=(3, 5), n_layers=2), dict(n_labels=1), dict(n_labels=35),
 ])
@@ -81,9 +82,16 @@ def test_res_config_overrides(override):
 
 
 def test_res_unsupported_width_fails_loudly():
+    """Beyond the kernels' envelope the forward raises (no silent fallback): more than
+    64 maps in f32, more than 48 in bf16 / bf16x3."""
+    cfg = dict(ref_configs()["res8"], n_feature_maps=65)
+    m = hm.find_model("res8")(cfg).eval().to(DEV)
+    with pytest.raises(RuntimeError, match="64 maps"):
+        m(torch.zeros(1, 101, 40, device=DEV))
     cfg = dict(ref_configs()["res8"], n_feature_maps=64)
     m = hm.find_model("res8")(cfg).eval().to(DEV)
-    with pytest.raises(RuntimeError, match="not supported"):
+    m.honk_precision = "bf16x3"
+    with pytest.raises(RuntimeError, match="48 in bf16"):
         m(torch.zeros(1, 101, 40, device=DEV))
 
 
