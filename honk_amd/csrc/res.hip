@@ -747,8 +747,16 @@ static int bands_w(const Layout& L, const honk_res_desc* d, int SP, int i) {
 // measured faster (45 maps at bf16x3: res15 2.14 vs 2.21 ms per 4096-clip
 // launch; it loses 7-20 % on the narrow, pooled and bf16 configurations), the
 // row-band one elsewhere.  HONK_RES_KERNEL=w / r forces either (tests run both).
+struct PairPlan {
+  bool ok;
+  int lag, NRA, NRB, slotb, ppr, ppw;  // ppw: DMA pieces per A wave per step
+};
+static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t n, int grid, int i);
 static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
-  bool want = L.NT == 3 && SP == 2;
+  // 45-map bf16x3: the weight-stationary path (with fused pairs); bf16: only when
+  // pairs fuse (the single weight-stationary layer is slower than the row-band one)
+  // (measured: res15 bf16 +4 %; res8's 13-pixel rows lose 20 % -- row-band there)
+  bool want = L.NT == 3 && (SP == 2 || (L.W >= 32 && L.L >= 3 && pair_at(L, d, SP, 4096, 256, 1).ok));
   if (const char* e = getenv("HONK_RES_KERNEL")) {
     if (e[0] == 'r') return false;
     if (e[0] == 'w') want = true;
@@ -765,10 +773,6 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
 // Fused pair plan (res_bf16p.inc) for layers A (dilation d) and B (tap stride sB
 // class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
-struct PairPlan {
-  bool ok;
-  int lag, NRA, NRB, slotb, ppr, ppw;  // ppw: DMA pieces per A wave per step
-};
 static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw) {
   PairPlan pp{false, 0, 0, 0, 0, 0, 0};
   const int P = 64, W = L.W, H = L.H;
@@ -841,19 +845,24 @@ static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw) {
 // workgroups, or ok = false: i odd, i + 1 not the last layer (the pair kernel has
 // no channel-sum epilogue), B's dilation d or 2d of A's, 45-map class bf16x3 on the
 // weight-stationary path, an instantiated row pitch, a plan that fits the LDS.
+// instantiated block16p_kernel<3, SP, PPR, PPW> (W = 40: res15, 20: res26 2x2 pool,
+// 13: res8 4x3 pool) -- the plan's pieces per wave may be fewer than PPW
+static int pair_ppw(int SP, int ppr) {
+  if (SP == 2) return ppr == 9 ? 9 : ppr == 5 ? 10 : ppr == 3 ? 9 : 0;
+  return ppr == 4 ? 4 : ppr == 2 ? 5 : 0;
+}
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t n, int grid, int i) {
   const PairPlan no{false, 0, 0, 0, 0, 0, 0};
   const char* kenv = getenv("HONK_RES_KERNEL");
-  if (L.NT != 3 || SP != 2 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
+  if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
   if (i % 2 == 0 || i + 1 >= L.L) return no;
   const int dA = dil_of(d, i), dB = dil_of(d, i + 1);
   const int sB = dB == dA ? 1 : (dB == 2 * dA ? 2 : 0);
   const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
   if (!sB || cb >= 0xE0000000ull) return no;
   const PairPlan pp = plan_pair(L, SP, dA, sB, (int)cdiv(n, grid));
-  // instantiated pitches: W = 40 (res15), 20 (res26, 2x2 pool), 13 (res8, 4x3 pool)
-  const bool inst = (pp.ppr == 9 && pp.ppw <= 9) || (pp.ppr == 5 && pp.ppw <= 10) || (pp.ppr == 3 && pp.ppw <= 9);
-  return pp.ok && inst ? pp : no;
+  const int ppw = pair_ppw(SP, pp.ppr);
+  return pp.ok && ppw && pp.ppw <= ppw ? pp : no;
 }
 
 template <int NT, int SP>
@@ -997,8 +1006,10 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
             Block16PArgs pa;
             pa.R = R;
-            pa.wA = (const char*)(packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats);
-            pa.wB = (const char*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats);
+            const float* fr = SP == 2 ? packed + L.off_fragx3 : packed + L.off_frag16;
+            const size_t fl = SP == 2 ? L.fragx3_floats : L.frag16_floats;
+            pa.wA = (const char*)(fr + (size_t)(i - 1) * fl);
+            pa.wB = (const char*)(fr + (size_t)i * fl);
             pa.chunk_bytes = (unsigned)cb;
             pa.nclips = (int)n;
             pa.H = L.H;
@@ -1013,9 +1024,12 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.slotb = pp.slotb;
             pa.ppr = pp.ppr;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
-            if (pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9>), dim3(grid), dim3(256), 0, st, pa);
-            else if (pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10>), dim3(grid), dim3(256), 0, st, pa);
-            else hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9>), dim3(grid), dim3(256), 0, st, pa);
+            const dim3 gd(grid), bd(256);
+            if (SP == 2 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9>), gd, bd, 0, st, pa);
+            else if (SP == 2 && pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10>), gd, bd, 0, st, pa);
+            else if (SP == 2) hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9>), gd, bd, 0, st, pa);
+            else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4>), gd, bd, 0, st, pa);
+            else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5>), gd, bd, 0, st, pa);
             HONK_LAUNCH_CHECK("res block16p_kernel");
             tl.done(st);
             ++i;  // layer i + 1 done too

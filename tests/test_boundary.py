@@ -228,10 +228,10 @@ def test_legacy_checkpoint_without_num_batches_tracked(tmp_path):
 
 def test_res_launch_plan_host_only(monkeypatch):
     """honk_res_launch_plan (host-only): which block kernels a forward launches per
-    chunk -- res15 bf16x3: six fused odd/even pairs then the last layer on the
-    weight-stationary kernel; res26 likewise (last pair unfused: the pair kernel has
-    no channel-sum epilogue); HONK_RES_KERNEL=w / r force single layers; f32 and
-    19-map bf16x3 keep their kernels."""
+    chunk -- res15 bf16x3 and bf16: six fused odd/even pairs then the last layer on
+    the weight-stationary kernel; res26 likewise (last pair unfused: the pair kernel
+    has no channel-sum epilogue); HONK_RES_KERNEL=w / r force single layers; f32 and
+    19-map models keep their kernels."""
     from honk_amd import _native
     from honk_amd import model as hm
     lib = _native.load()
@@ -250,7 +250,8 @@ def test_res_launch_plan_host_only(monkeypatch):
     assert plan("res26", "bf16x3") == ["block16p_kernel"] * 11 + ["block16w_kernel"] * 2
     assert plan("res8", "bf16x3") == ["block16p_kernel"] * 2 + ["block16w_kernel"] * 2
     assert plan("res15", "f32") == ["block_kernel"] * 13
-    assert plan("res15", "bf16") == ["block16r_kernel"] * 13
+    assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16w_kernel"]
+    assert plan("res8", "bf16") == ["block16r_kernel"] * 6  # 13-pixel rows: row-band measured faster
     assert plan("res15-narrow", "bf16x3") == ["block16r_kernel"] * 13
     monkeypatch.setenv("HONK_RES_KERNEL", "w")
     assert plan("res15", "bf16x3") == ["block16w_kernel"] * 13
