@@ -111,6 +111,8 @@ PAIR_CASES = [("res15", {}, 600), ("res15", dict(n_feature_maps=33), 300), ("res
 def test_pair_kernel_bitwise_vs_w(monkeypatch, name, override, B, prec):
     cfg = dict(ref_configs()[name])
     cfg.update(override)
+    if prec == "bf16" and "res_pool" in cfg:
+        pytest.skip("bf16 pairs run on full-width (40-pixel) rows only; pooled bf16 stays on the row-band kernel")
     params, x = _case(cfg, B, seed=31)
     m = _module(cfg, params, name, prec)
     monkeypatch.setenv("HONK_RES_KERNEL", "p")
