@@ -111,6 +111,62 @@ class _BatchNormTrain(torch.autograd.Function):
         return dx, None, None, None, None
 
 
+class _ResTail(torch.autograd.Function):
+    """s = relu(h) [+ old]; y = BatchNorm_train(s) on honk_res_tail_fwd/bwd_f32
+    (model.py:111-118): returns y, or (y, s) when s feeds the next residual."""
+
+    @staticmethod
+    def forward(ctx, h, old, running_mean, running_var, momentum, eps, keep_s):
+        h = h.contiguous()
+        old = old.contiguous() if old is not None else None
+        B, C, H, W = h.shape
+        y = torch.empty_like(h)
+        s = torch.empty_like(h) if keep_s else None
+        mean = torch.empty(C, dtype=torch.float32, device=h.device)
+        invstd = torch.empty_like(mean)
+        ws, nb = _bn_ws(B, C, H * W, h.device)
+        ptr = (lambda t: t.data_ptr() if t is not None else None)
+        _native.check(_native.load().honk_res_tail_fwd_f32(h.data_ptr(), ptr(old), ptr(s), y.data_ptr(),
+                                                           mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
+                                                           ptr(running_var), B, C, H * W, momentum, eps,
+                                                           ws.data_ptr(), nb, _native.stream_handle(h.device)),
+                      "honk_res_tail_fwd_f32")
+        ctx.save_for_backward(h, y, invstd)
+        ctx.has_old = old is not None
+        if keep_s:
+            return y, s
+        return y
+
+    @staticmethod
+    def backward(ctx, gy, gs=None):
+        h, y, invstd = ctx.saved_tensors
+        B, C, H, W = y.shape
+        if gy is None:
+            gy = torch.zeros_like(y)
+        gy = gy.contiguous()
+        gs = gs.contiguous() if gs is not None else None
+        gh = torch.empty_like(y)
+        gold = torch.empty_like(y) if ctx.has_old and ctx.needs_input_grad[1] else None
+        ws, nb = _bn_ws(B, C, H * W, y.device)
+        ptr = (lambda t: t.data_ptr() if t is not None else None)
+        _native.check(_native.load().honk_res_tail_bwd_f32(gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(),
+                                                           h.data_ptr(), gh.data_ptr(), ptr(gold), B, C, H * W,
+                                                           ws.data_ptr(), nb, _native.stream_handle(y.device)),
+                      "honk_res_tail_bwd_f32")
+        return gh, gold, None, None, None, None, None
+
+
+def res_tail(h, old, bn, keep_s=False):
+    """The res block tail in training (model.py:111-118): x = relu(h); x = x + old
+    (old not None); old_x = x; x = bn(x) -- one native kernel chain, bit-identical
+    to the unfused PyTorch ops.  Returns bn's output, or (output, old_x) if keep_s."""
+    bn.num_batches_tracked.add_(1)
+    out = _ResTail.apply(h, old, bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps), bool(keep_s))
+    torch.autograd.graph.increment_version(bn.running_mean)
+    torch.autograd.graph.increment_version(bn.running_var)
+    return out
+
+
 def bn_supported(x, bn) -> bool:
     return (x.is_cuda and x.dtype == torch.float32 and bn.training and not bn.affine
             and bn.track_running_stats and bn.momentum is not None and x.shape[0] > 1)

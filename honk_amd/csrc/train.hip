@@ -467,6 +467,150 @@ __global__ __launch_bounds__(512) void wgrad3x3_kernel(WgradArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------- //
+// wgrad3x3m_kernel<C> (C <= 20): the weight gradient on v_mfma_f32_16x16x4_f32 as
+// a GEMM D[o][j] = sum_p dy[o][p] X[j][p] over the tile's pixels p (k of the MFMA),
+// j = 9 ci + t (input channel, tap) -- the [o][ci][t] layout of dW.  M = output
+// channels (C -> 2 tiles of 16), N = 9C columns (171 -> 11 tiles), so one wave holds
+// 22 accumulator tiles and reads 2 A + 11 B floats per 4 pixels (22 MFMAs).  A band of
+// TH class rows is staged as in conv3x3m_kernel (x with a one-row / d-column zero
+// halo at a fixed plane stride; dy as [o][TH W]), 2 workgroups per CU so one
+// stages while the other multiplies.  The 4 waves take interleaved k-steps; their
+// partials are summed in LDS in wave order and each workgroup writes one partial
+// dW, which wsum_kernel adds in a fixed order (deterministic, no atomics).
+// ---------------------------------------------------------------------------- //
+constexpr int TW_XL = 36 * 1024, TW_DL = 28 * 1024;  // staged x / dy bytes per workgroup
+
+template <int C>
+__global__ __launch_bounds__(256, 2) void wgrad3x3m_kernel(WgradArgs a) {
+  static_assert(C <= 20, "wgrad3x3m_kernel: C <= 20");
+  constexpr int K9 = 9 * C, NJ = (K9 + 15) / 16, NO = (C + 15) / 16;
+  __shared__ __attribute__((aligned(16))) float lds[(TW_XL + TW_DL) / 4];
+  float* xl = lds;
+  float* dl = lds + TW_XL / 4;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int d = a.g.d, Wp = a.W + 2 * d, TH = a.g.TH;
+  const int R = TH + 2, PS = R * Wp, DS = TH * a.W;  // x plane stride, dy plane stride
+  int joff[NJ];  // B lanes: LDS offset of column j = 16 n + i16 (pad columns read plane 0)
+#pragma unroll
+  for (int n = 0; n < NJ; ++n) {
+    const int j = 16 * n + i16, ci = j / 9, t = j - 9 * ci;
+    joff[n] = j < K9 ? ci * PS + (t / 3) * Wp + (t % 3) * d : 0;
+  }
+  f32x4_t acc[NO][NJ];
+#pragma unroll
+  for (int m = 0; m < NO; ++m)
+#pragma unroll
+    for (int n = 0; n < NJ; ++n) acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // halo columns zeroed once (every tile writes only the W interior columns)
+  for (int i = tid; i < C * R * 2 * d; i += 256) {
+    const int row = i / (2 * d), e = i - row * (2 * d);
+    const int c = row / R, rr = row - c * R;
+    xl[c * PS + rr * Wp + (e < d ? e : a.W + e)] = 0.f;
+  }
+  const int SR = 256 / a.W, rl0 = tid / a.W, col0 = tid - rl0 * a.W;
+  const float invR = 1.0f / (float)R, invT = 1.0f / (float)TH;
+  for (int tile = blockIdx.x; tile < a.B * a.g.nband; tile += gridDim.x) {
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, a.H, tile - b * a.g.nband, r, k0, th);
+    __syncthreads();  // previous tile's readers done
+    if (rl0 < SR) {
+      const float* xb = a.x + (size_t)b * C * a.H * a.W + col0;
+      for (int row0 = rl0; row0 < C * R; row0 += 8 * SR) {  // 8 loads in flight per thread
+        float v[8];
+        int dst[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int row = row0 + u * SR;
+          int c = (int)((float)row * invR);  // exact after the +-1 fix-up: row < 2^16 (host-checked)
+          c += (row - c * R >= R) ? 1 : ((row - c * R < 0) ? -1 : 0);
+          const int rr = row - c * R;
+          const int h = r + (k0 - 1 + rr) * d;
+          v[u] = (row < C * R && h >= 0 && h < a.H) ? xb[((size_t)c * a.H + h) * a.W] : 0.f;
+          dst[u] = row < C * R ? c * PS + rr * Wp + d + col0 : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (dst[u] >= 0) xl[dst[u]] = v[u];
+      }
+      const float* db = a.dy + (size_t)b * C * a.H * a.W + col0;
+      for (int row0 = rl0; row0 < C * TH; row0 += 8 * SR) {
+        float v[8];
+        int dst[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int row = row0 + u * SR;
+          int o = (int)((float)row * invT);
+          o += (row - o * TH >= TH) ? 1 : ((row - o * TH < 0) ? -1 : 0);
+          const int jr = row - o * TH;
+          const int h = r + (k0 + jr) * d;
+          v[u] = (row < C * TH && jr < th) ? db[((size_t)o * a.H + h) * a.W] : 0.f;
+          dst[u] = row < C * TH ? o * DS + jr * a.W + col0 : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (dst[u] >= 0) dl[dst[u]] = v[u];
+      }
+    }
+    __syncthreads();
+    const int npx = th * a.W, nks = (npx + 3) >> 2;
+    for (int s = wave; s < nks; s += 4) {
+      const int p = 4 * s + kk;
+      const bool pv = p < npx;  // k beyond the band: A = 0 (B reads pixel 0, finite)
+      const int pp = pv ? p : 0;
+      const int row = pp / a.W, col = pp - row * a.W;
+      const float* xp = xl + row * Wp + col;
+      float av[NO], bv[NJ];
+#pragma unroll
+      for (int m = 0; m < NO; ++m) {
+        const int o = 16 * m + i16;
+        av[m] = (pv && o < C) ? dl[o * DS + pp] : 0.f;
+      }
+#pragma unroll
+      for (int n = 0; n < NJ; ++n) bv[n] = xp[joff[n]];
+#pragma unroll
+      for (int m = 0; m < NO; ++m)
+#pragma unroll
+        for (int n = 0; n < NJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+  }
+  // the 4 waves' partials summed in wave order, one 16-row output tile at a time:
+  // red[w][i][j], i = row in the tile (lane (j, g) holds rows 4 g .. 4 g + 3)
+  float* pb = a.part + (size_t)blockIdx.x * C * K9;
+  constexpr int NJP = NJ * 16;
+#pragma unroll
+  for (int m = 0; m < NO; ++m) {
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < NJ; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lds[(wave * 16 + 4 * kk + i) * NJP + 16 * n + i16] = acc[m][n][i];
+    __syncthreads();
+    for (int idx = tid; idx < 16 * K9; idx += 256) {
+      const int i = idx / K9, j = idx - i * K9, o = 16 * m + i;
+      const float v = ((lds[i * NJP + j] + lds[(16 + i) * NJP + j]) + lds[(32 + i) * NJP + j]) + lds[(48 + i) * NJP + j];
+      if (o < C) pb[o * K9 + j] = v;
+    }
+  }
+}
+
+// class rows per wgrad3x3m_kernel tile: C x planes of (TH + 2) x (W + 2d) in TW_XL,
+// C dy planes of TH x W in TW_DL, the 4 waves' 64 x 16 NJ partial sums in both
+static int tw_rows(int C, int H, int W, int d) {
+  const int Wp = W + 2 * d;
+  int th = TW_XL / 4 / C / Wp - 2;
+  const int byd = TW_DL / 4 / C / W;
+  if (th > byd) th = byd;
+  const int hc = (H + d - 1) / d;
+  if (th > hc) th = hc;
+  if (th < 1 || W > 256 || (long)C * (th + 2) * Wp >= 65536) return 0;
+  const int nb = (hc + th - 1) / th;
+  return (hc + nb - 1) / nb;
+}
+
 // dw[i] = sum over the nblk per-workgroup partials, fixed order: 64 outputs per
 // workgroup, 4 strands over k (k = strand mod 4) combined in LDS
 __global__ __launch_bounds__(256) void wsum_kernel(const float* __restrict__ part, float* __restrict__ dw, int n,
@@ -603,6 +747,119 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   out[i] = b ? v[c] * (a[i] - u[c] - b[i] * w[c]) : (a[i] - u[c]) * v[c];
 }
 
+// ---------------------------------------------------------------------------- //
+// The res block tail fused around the train-mode BatchNorm (model.py:111-118):
+//   s = relu(h) [+ old]   (h = the block conv's output, old = the residual stream)
+//   y = (s - mean) * invstd, batch statistics of s
+// and its backward
+//   g = invstd (gy - mean(gy) - y mean(gy y)) [+ gs]   (gs: grad of s as the next residual)
+//   gold = g,  gh = g where h > 0 else 0
+// so that ReLU, the residual add, its gradient accumulation and ReLU's backward
+// never round-trip HBM on their own.  Every value is the same fp32 operation the
+// unfused PyTorch graph performs (relu, add, BatchNorm kernels above, autograd's
+// accumulation, threshold_backward): bit-identical to it.
+// ---------------------------------------------------------------------------- //
+__device__ __forceinline__ float relu_f(float h) { return h <= 0.f ? 0.f : h; }  // NaN passes, as torch.relu
+
+__global__ __launch_bounds__(256) void tail_partial_kernel(const float* __restrict__ h, const float* __restrict__ old,
+                                                           double* __restrict__ part, int B, int C, int HW, int S) {
+  __shared__ double red[4];
+  const int c = blockIdx.x, s = blockIdx.y;
+  const int b0 = (int)((int64_t)B * s / S), b1 = (int)((int64_t)B * (s + 1) / S);
+  double sa = 0.0, sab = 0.0;
+  if ((HW & 3) == 0) {
+    const int hw4 = HW >> 2;
+    const int n4 = (b1 - b0) * hw4;
+    for (int k = threadIdx.x; k < n4; k += 256) {
+      const int pl = k / hw4, o4 = k - pl * hw4;
+      const size_t off = ((size_t)(b0 + pl) * C + c) * HW + 4 * o4;
+      const float4 hv = *(const float4*)(h + off);
+      float4 a = float4{relu_f(hv.x), relu_f(hv.y), relu_f(hv.z), relu_f(hv.w)};
+      if (old) {
+        const float4 ov = *(const float4*)(old + off);
+        a = float4{a.x + ov.x, a.y + ov.y, a.z + ov.z, a.w + ov.w};
+      }
+      sa += (double)((a.x + a.y) + (a.z + a.w));
+      sab += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
+    }
+  } else {
+    for (int b = b0; b < b1; ++b) {
+      const size_t base = ((size_t)b * C + c) * HW;
+      for (int i = threadIdx.x; i < HW; i += 256) {
+        float a = relu_f(h[base + i]);
+        if (old) a = a + old[base + i];
+        sa += (double)a;
+        sab += (double)a * (double)a;
+      }
+    }
+  }
+  sa = bn_block_sum(sa, red);
+  sab = bn_block_sum(sab, red);
+  if (threadIdx.x == 0) {
+    part[((size_t)c * S + s) * 2] = sa;
+    part[((size_t)c * S + s) * 2 + 1] = sab;
+  }
+}
+
+// y = (relu(h) [+ old] - mean[c]) * invstd[c]; s_out (may be null) = relu(h) [+ old]
+__global__ __launch_bounds__(256) void tail_fwd_kernel(const float* __restrict__ h, const float* __restrict__ old,
+                                                       const float* __restrict__ u, const float* __restrict__ v,
+                                                       float* __restrict__ y, float* __restrict__ s_out, int64_t total,
+                                                       int C, int HW) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((HW & 3) == 0) {
+    const int64_t i4 = 4 * i;
+    if (i4 >= total) return;
+    const int c = (int)((i4 / HW) % C);
+    const float4 hv = *(const float4*)(h + i4);
+    float4 a = float4{relu_f(hv.x), relu_f(hv.y), relu_f(hv.z), relu_f(hv.w)};
+    if (old) {
+      const float4 ov = *(const float4*)(old + i4);
+      a = float4{a.x + ov.x, a.y + ov.y, a.z + ov.z, a.w + ov.w};
+    }
+    if (s_out) *(float4*)(s_out + i4) = a;
+    *(float4*)(y + i4) = float4{(a.x - u[c]) * v[c], (a.y - u[c]) * v[c], (a.z - u[c]) * v[c], (a.w - u[c]) * v[c]};
+    return;
+  }
+  if (i >= total) return;
+  const int c = (int)((i / HW) % C);
+  float a = relu_f(h[i]);
+  if (old) a = a + old[i];
+  if (s_out) s_out[i] = a;
+  y[i] = (a - u[c]) * v[c];
+}
+
+// g = v[c] (gy - u[c] - y w[c]) [+ gs]; gold (may be null) = g; gh = h > 0 ? g : 0
+__global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+                                                       const float* __restrict__ gs, const float* __restrict__ h,
+                                                       const float* __restrict__ u, const float* __restrict__ v,
+                                                       const float* __restrict__ w, float* __restrict__ gh,
+                                                       float* __restrict__ gold, int64_t total, int C, int HW) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((HW & 3) == 0) {
+    const int64_t i4 = 4 * i;
+    if (i4 >= total) return;
+    const int c = (int)((i4 / HW) % C);
+    const float4 av = *(const float4*)(gy + i4), bv = *(const float4*)(y + i4), hv = *(const float4*)(h + i4);
+    float4 g = float4{v[c] * (av.x - u[c] - bv.x * w[c]), v[c] * (av.y - u[c] - bv.y * w[c]),
+                      v[c] * (av.z - u[c] - bv.z * w[c]), v[c] * (av.w - u[c] - bv.w * w[c])};
+    if (gs) {
+      const float4 sv = *(const float4*)(gs + i4);
+      g = float4{g.x + sv.x, g.y + sv.y, g.z + sv.z, g.w + sv.w};
+    }
+    if (gold) *(float4*)(gold + i4) = g;
+    *(float4*)(gh + i4) = float4{hv.x <= 0.f ? 0.f : g.x, hv.y <= 0.f ? 0.f : g.y, hv.z <= 0.f ? 0.f : g.z,
+                                 hv.w <= 0.f ? 0.f : g.w};
+    return;
+  }
+  if (i >= total) return;
+  const int c = (int)((i / HW) % C);
+  float g = v[c] * (gy[i] - u[c] - y[i] * w[c]);
+  if (gs) g = g + gs[i];
+  if (gold) gold[i] = g;
+  gh[i] = h[i] <= 0.f ? 0.f : g;
+}
+
 static int bn_slices(int B, int C) {
   int S = (4 * 256 + C - 1) / C;  // ~4 workgroups per CU in total
   if (S > B) S = B;
@@ -695,12 +952,33 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   return HONK_OK;
 }
 
+namespace {
+// the weight-gradient kernel for a shape: the MFMA one for 19 maps (HONK_TRAIN_CONV=v
+// selects the VALU kernel, for tests), its class-band geometry and grid
+struct WgradPlan {
+  bool mfma;
+  train::ClassBands g;
+  int grid;
+};
+WgradPlan wgrad_plan(int64_t batch, int c, int h, int w_, int dil) {
+  WgradPlan p;
+  const char* ke = getenv("HONK_TRAIN_CONV");
+  const int tw = c == 19 && !(ke && ke[0] == 'v') ? train::tw_rows(c, h, w_, dil) : 0;
+  p.mfma = tw > 0;
+  p.g = train::class_bands(h, dil, p.mfma ? tw : train::tc_rows(c, h, w_, dil));
+  p.grid = train::tc_grid(batch * p.g.nband);
+  return p;
+}
+}  // namespace
+
 extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil) {
   if (batch < 1 || (c != 19 && c != 45) || h < 1 || w_ < 1 || dil < 1 || dil > 64) return 0;
-  const int th = train::tc_rows(c, h, w_, dil);
-  if (th < 1) return 0;
-  const int64_t tiles = batch * train::class_bands(h, dil, th).nband;
-  return (size_t)train::tc_grid(tiles) * c * c * 9 * sizeof(float);
+  if (train::tc_rows(c, h, w_, dil) < 1) return 0;
+  // either kernel's grid (the environment may switch kernels between this query and the call)
+  const int64_t t0 = batch * train::class_bands(h, dil, train::tc_rows(c, h, w_, dil)).nband;
+  const int tw = c == 19 ? train::tw_rows(c, h, w_, dil) : 0;
+  const int64_t t1 = tw > 0 ? batch * train::class_bands(h, dil, tw).nband : 0;
+  return (size_t)train::tc_grid(t0 > t1 ? t0 : t1) * c * c * 9 * sizeof(float);
 }
 
 extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
@@ -719,10 +997,12 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
   train::WgradArgs a;
   a.x = x; a.dy = dy; a.part = (float*)workspace;
   a.B = (int)batch; a.H = h; a.W = w_;
-  a.g = train::class_bands(h, dil, train::tc_rows(c, h, w_, dil));
-  const int grid = train::tc_grid((int64_t)a.B * a.g.nband);
+  const WgradPlan wp = wgrad_plan(batch, c, h, w_, dil);
+  a.g = wp.g;
+  const int grid = wp.grid;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(512), 0, st, a);
+  if (wp.mfma) hipLaunchKernelGGL((train::wgrad3x3m_kernel<19>), dim3(grid), dim3(256), 0, st, a);
+  else if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((train::wgrad3x3_kernel<45>), dim3(grid), dim3(512), 0, st, a);
   tl.done(st);
   HONK_LAUNCH_CHECK("wgrad3x3_kernel");
@@ -782,5 +1062,52 @@ extern "C" int honk_bn_train_bwd_f32(const float* dy, const float* y, const floa
   hipLaunchKernelGGL(train::bn_apply_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, dy, y,
                      (const float*)m, invstd, (const float*)(m + c), dx, total, c, (int)hw);
   HONK_LAUNCH_CHECK("bn_apply_kernel");
+  return HONK_OK;
+}
+
+extern "C" int honk_res_tail_fwd_f32(const float* h, const float* old, float* s, float* y, float* mean, float* invstd,
+                                     float* running_mean, float* running_var, int64_t batch, int32_t c, int64_t hw,
+                                     float momentum, float eps, void* workspace, size_t ws_bytes, void* stream) {
+  if (!h || !y || !mean || !invstd || (!running_mean != !running_var)) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 1 || c < 1 || hw < 1 || hw > 0x7fffffff || batch > 0x7fffffff) return fail(HONK_ERR_ARG, "bad batchnorm shape");
+  const size_t need = honk_bn_train_workspace_bytes(batch, c, hw);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  const int S = train::bn_slices((int)batch, c);
+  double* part = (double*)workspace;
+  hipLaunchKernelGGL(train::tail_partial_kernel, dim3(c, S), dim3(256), 0, st, h, old, part, (int)batch, c, (int)hw, S);
+  HONK_LAUNCH_CHECK("tail_partial_kernel");
+  hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)cdiv(c, 64)), dim3(64), 0, st, (const double*)part, mean,
+                     invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
+  HONK_LAUNCH_CHECK("bn_stats_kernel");
+  const int64_t total = batch * c * hw;
+  const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
+  hipLaunchKernelGGL(train::tail_fwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, h, old,
+                     (const float*)mean, (const float*)invstd, y, s, total, c, (int)hw);
+  HONK_LAUNCH_CHECK("tail_fwd_kernel");
+  return HONK_OK;
+}
+
+extern "C" int honk_res_tail_bwd_f32(const float* gy, const float* gs, const float* y, const float* invstd,
+                                     const float* h, float* gh, float* gold, int64_t batch, int32_t c, int64_t hw,
+                                     void* workspace, size_t ws_bytes, void* stream) {
+  if (!gy || !y || !invstd || !h || !gh) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 1 || c < 1 || hw < 1 || hw > 0x7fffffff || batch > 0x7fffffff) return fail(HONK_ERR_ARG, "bad batchnorm shape");
+  const size_t need = honk_bn_train_workspace_bytes(batch, c, hw);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  const int S = train::bn_slices((int)batch, c);
+  double* part = (double*)workspace;
+  float* m = (float*)(part + (size_t)c * S * 2);
+  hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, gy, y, part, (int)batch, c, (int)hw, S);
+  HONK_LAUNCH_CHECK("bn_partial_kernel");
+  hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)cdiv(c, 64)), dim3(64), 0, st, (const double*)part, m,
+                     m + c, c, S, (double)batch * (double)hw);
+  HONK_LAUNCH_CHECK("bn_bstats_kernel");
+  const int64_t total = batch * c * hw;
+  const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
+  hipLaunchKernelGGL(train::tail_bwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
+                     (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
+  HONK_LAUNCH_CHECK("tail_bwd_kernel");
   return HONK_OK;
 }

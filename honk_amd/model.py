@@ -162,6 +162,18 @@ class SpeechResModel(SerializableModule):
         x = x.unsqueeze(1)
         for i in range(self.n_layers + 1):
             conv = getattr(self, "conv{}".format(i))
+            if native_convs and i > 0 and _conv3x3.supported(x, conv) and \
+                    _conv3x3.bn_supported(x, getattr(self, "bn{}".format(i))):
+                # conv, then relu / residual add / train BatchNorm as one fused tail
+                h = _conv3x3.conv3x3(x, conv.weight, conv.dilation[0])
+                bn = getattr(self, "bn{}".format(i))
+                if i % 2 == 0:
+                    keep = i + 2 <= self.n_layers  # old_x is read again by layer i + 2
+                    out = _conv3x3.res_tail(h, old_x, bn, keep_s=keep)
+                    x, old_x = out if keep else (out, None)
+                else:
+                    x = _conv3x3.res_tail(h, None, bn)
+                continue
             if native_convs and i > 0 and _conv3x3.supported(x, conv):
                 y = F.relu(_conv3x3.conv3x3(x, conv.weight, conv.dilation[0]))
             else:

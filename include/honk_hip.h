@@ -181,6 +181,24 @@ int honk_bn_train_fwd_f32(const float* x, float* y, float* mean, float* invstd, 
                           void* workspace, size_t workspace_bytes, void* stream);
 int honk_bn_train_bwd_f32(const float* dy, const float* y, const float* invstd, float* dx, int64_t batch,
                           int32_t c, int64_t hw, void* workspace, size_t workspace_bytes, void* stream);
+/*
+ * The res block tail around that BatchNorm, fused (model.py:111-118 in training:
+ * x = relu(conv(x)); x = x + old_x on even layers; x = bn(x)), replacing the
+ * relu / add / BatchNorm2d / threshold_backward / gradient-accumulation kernels
+ * autograd runs for it (utils/train.py:131-134):
+ *   forward:  s = relu(h) [+ old]  (old may be NULL; s written only when non-NULL),
+ *             y = (s - mean) * invstd, batch statistics of s, running stats as above;
+ *   backward: g = invstd * (gy - mean(gy) - y * mean(gy * y)) [+ gs]  (gs may be NULL:
+ *             the gradient of s through its use as the next residual),
+ *             gold = g (may be NULL), gh = (h > 0 ? g : 0).
+ * Bit-identical to the unfused operations.  Workspace: honk_bn_train_workspace_bytes.
+ */
+int honk_res_tail_fwd_f32(const float* h, const float* old, float* s, float* y, float* mean, float* invstd,
+                          float* running_mean, float* running_var, int64_t batch, int32_t c, int64_t hw,
+                          float momentum, float eps, void* workspace, size_t workspace_bytes, void* stream);
+int honk_res_tail_bwd_f32(const float* gy, const float* gs, const float* y, const float* invstd, const float* h,
+                          float* gh, float* gold, int64_t batch, int32_t c, int64_t hw, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* ---- diagnostics --------------------------------------------------------------- */
 const char* honk_last_error(void);

@@ -141,9 +141,51 @@ def test_conv3x3_mfma_bitwise_vs_valu(monkeypatch, B, H, W, d):
     g = torch.Generator(device=DEV).manual_seed(7 + H + d)
     x = torch.randn(B, 19, H, W, device=DEV, generator=g)
     w = torch.randn(19, 19, 3, 3, device=DEV, generator=g) * 0.1
+    dy = torch.randn(B, 19, H, W, device=DEV, generator=g)
     outs = {}
     for k in ("m", "v"):
         monkeypatch.setenv("HONK_TRAIN_CONV", k)
-        outs[k] = (hc._conv(x, w, flip=False, d=d), hc._conv(x, w, flip=True, d=d))
+        outs[k] = (hc._conv(x, w, flip=False, d=d), hc._conv(x, w, flip=True, d=d), hc._wgrad(x, dy, d=d))
     assert torch.equal(outs["m"][0], outs["v"][0])
     assert torch.equal(outs["m"][1], outs["v"][1])
+    # the weight gradient (wgrad3x3m_kernel) sums the pixels in another order: fp32
+    # rounding apart, the same sums (both are within 1e-5 of float64 above)
+    assert _rel(outs["m"][2], outs["v"][2]) < 1e-5
+
+
+@pytest.mark.parametrize("B,C,H,W,res,keep", [(64, 19, 50, 20, True, True), (64, 19, 50, 20, False, False),
+                                              (5, 45, 25, 13, True, False), (3, 19, 101, 40, True, True),
+                                              (2, 19, 7, 5, False, False)])
+def test_res_tail_bitwise_vs_unfused(B, C, H, W, res, keep):
+    """honk_res_tail_fwd/bwd_f32 (relu, residual add, train BatchNorm, their backward
+    and the residual gradient accumulation in one kernel chain) vs the same ops run
+    one by one (F.relu, +, honk_bn_train_*, autograd): bit-identical outputs, running
+    stats and gradients, for float4 (HW % 4 == 0) and scalar (res8's 25x13) planes."""
+    g = torch.Generator(device=DEV).manual_seed(B * 7 + C + H)
+    h = torch.randn(B, C, H, W, device=DEV, generator=g)
+    old = torch.randn(B, C, H, W, device=DEV, generator=g) if res else None
+    gy = torch.randn(B, C, H, W, device=DEV, generator=g)
+    gs = torch.randn(B, C, H, W, device=DEV, generator=g) if keep else None
+
+    def run(fused):
+        hh = h.clone().requires_grad_(True)
+        oo = old.clone().requires_grad_(True) if res else None
+        bn = torch.nn.BatchNorm2d(C, affine=False).to(DEV).train()
+        if fused:
+            out = hc.res_tail(hh, oo, bn, keep_s=keep)
+            y, s = out if keep else (out, None)
+        else:
+            s = F.relu(hh)
+            if res:
+                s = s + oo
+            y = hc.batch_norm_train(s, bn)
+        outs, grads = [y] + ([s] if keep else []), [gy] + ([gs] if keep else [])
+        ins = [hh] + ([oo] if res else [])
+        gr = torch.autograd.grad(outs, ins, grads)
+        return [t.detach() for t in outs] + list(gr) + [bn.running_mean.clone(), bn.running_var.clone(),
+                                                        bn.num_batches_tracked.clone()]
+
+    a, b = run(True), run(False)
+    assert len(a) == len(b)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), (i, float((u.double() - v.double()).abs().max()))
