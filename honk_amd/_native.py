@@ -71,7 +71,12 @@ _PROTOS = {
                                              ctypes.c_void_p]),
     "honk_res_tail_bwd_f32": (ctypes.c_int, [c_f32p] * 7 + [ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
                                              ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
-    "honk_mfcc_f32":(ctypes.c_int, [c_f32p, ctypes.c_int64, ctypes.c_int32, c_f32p, ctypes.c_int32, ctypes.c_int32,
+    "honk_res_stem_fwd_f32": (ctypes.c_int, [c_f32p] * 3 + [ctypes.c_int64] + [ctypes.c_int32] * 5
+                              + [ctypes.c_void_p]),
+    "honk_res_stem_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32]),
+    "honk_res_stem_wgrad_f32": (ctypes.c_int, [c_f32p] * 4 + [ctypes.c_int64] + [ctypes.c_int32] * 5
+                                + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_mfcc_f32": (ctypes.c_int, [c_f32p, ctypes.c_int64, ctypes.c_int32, c_f32p, ctypes.c_int32, ctypes.c_int32,
                                      c_f32p, ctypes.c_int32, c_f32p, ctypes.c_int32, c_f32p, ctypes.c_void_p]),
     "honk_last_error": (ctypes.c_char_p, []),
     "honk_version": (ctypes.c_char_p, []),

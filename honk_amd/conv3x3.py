@@ -183,3 +183,62 @@ def batch_norm_train(x, bn):
     torch.autograd.graph.increment_version(bn.running_mean)
     torch.autograd.graph.increment_version(bn.running_var)
     return y
+
+
+# -- the res stem in training: relu(conv0(x)) [+ AvgPool2d] (model.py:104-110) --------
+class _Stem(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w0, ph, pw):
+        x, w0 = x.contiguous(), w0.contiguous()
+        B, H, W = x.shape
+        C = w0.shape[0]
+        y = torch.empty(B, C, H // ph, W // pw, dtype=torch.float32, device=x.device)
+        _native.check(_native.load().honk_res_stem_fwd_f32(x.data_ptr(), w0.data_ptr(), y.data_ptr(), B, C, H, W,
+                                                           ph, pw, _native.stream_handle(x.device)),
+                      "honk_res_stem_fwd_f32")
+        ctx.save_for_backward(x, w0)
+        ctx.pool = (ph, pw)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w0 = ctx.saved_tensors
+        ph, pw = ctx.pool
+        B, H, W = x.shape
+        C = w0.shape[0]
+        gy = gy.contiguous()
+        lib = _native.load()
+        dw = torch.empty_like(w0)
+        nb = int(lib.honk_res_stem_wgrad_workspace_bytes(B, C))
+        ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=x.device)
+        _native.check(lib.honk_res_stem_wgrad_f32(x.data_ptr(), w0.data_ptr(), gy.data_ptr(), dw.data_ptr(), B, C,
+                                                  H, W, ph, pw, ws.data_ptr(), nb, _native.stream_handle(x.device)),
+                      "honk_res_stem_wgrad_f32")
+        return None, dw, None, None
+
+
+def stem_supported(x, conv0, pool) -> bool:
+    """[B, H, W] fp32 input that needs no gradient, conv0 = Conv2d(1, C, 3, padding 1,
+    no bias), AvgPool2d with stride = kernel and no padding (or no pool)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and not x.requires_grad):
+        return False
+    if not (tuple(conv0.kernel_size) == (3, 3) and tuple(conv0.padding) == (1, 1) and conv0.bias is None
+            and tuple(conv0.stride) == (1, 1) and tuple(conv0.dilation) == (1, 1) and conv0.in_channels == 1
+            and 1 <= conv0.out_channels <= 64 and (x.shape[1] + 2) * (x.shape[2] + 2) <= 8192):
+        return False
+    if pool is None:
+        return True
+    k = pool.kernel_size if isinstance(pool.kernel_size, tuple) else (pool.kernel_size,) * 2
+    s = pool.stride if isinstance(pool.stride, tuple) else (pool.stride,) * 2
+    p = pool.padding if isinstance(pool.padding, tuple) else (pool.padding,) * 2
+    return (tuple(k) == tuple(s) and tuple(p) == (0, 0) and not pool.ceil_mode and pool.divisor_override is None
+            and k[0] <= x.shape[1] and k[1] <= x.shape[2])
+
+
+def stem(x, conv0, pool=None):
+    """y = pool(relu(conv0(x.unsqueeze(1)))) on honk_res_stem_fwd_f32 / wgrad_f32."""
+    if pool is None:
+        ph = pw = 1
+    else:
+        ph, pw = pool.kernel_size if isinstance(pool.kernel_size, tuple) else (pool.kernel_size,) * 2
+    return _Stem.apply(x, conv0.weight, int(ph), int(pw))

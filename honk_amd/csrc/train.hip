@@ -220,7 +220,64 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(Conv3Args a) {
 // operand (ceil(9C / 4) k-steps x 2 out-tiles floats per lane) stays in VGPRs;
 // two workgroups per CU.  Output lane (p, g) holds channels 16 n + 4 g .. +3.
 // ---------------------------------------------------------------------------- //
-constexpr int TM_XL = 64 * 1024;  // staged tile bytes
+constexpr int TM_XL = 64 * 1024;  // staged tile bytes (2 workgroups per CU; 3 would spill the weight operand)
+
+// Stage nrows image rows of W floats into LDS with the workgroup's 256 threads:
+// row i comes from src(i) (nullptr: zeros) and lands at LDS offset dst(i).  Each
+// thread keeps 8 loads in flight (the tile is latency-bound otherwise: a serial walk
+// waits out the HBM latency on every row); rows whose W is a multiple of 4 move as
+// float4s (16 B per lane, 4x the bytes in flight of the scalar walk).
+template <typename Src, typename Dst>
+__device__ __forceinline__ void stage_rows(float* __restrict__ lds, int nrows, int W, Src src, Dst dst) {
+  const int tid = threadIdx.x;
+  if ((W & 3) == 0) {
+    const int W4 = W >> 2, SR = 256 / W4, rl0 = tid / W4, c4 = 4 * (tid - rl0 * W4);
+    if (rl0 >= SR) return;
+    for (int row0 = rl0; row0 < nrows; row0 += 8 * SR) {
+      float4 v[8];
+      int o[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int row = row0 + u * SR;
+        const float* p = row < nrows ? src(row) : nullptr;
+        v[u] = p ? *(const float4*)(p + c4) : float4{0.f, 0.f, 0.f, 0.f};
+        o[u] = row < nrows ? dst(row) + c4 : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (o[u] >= 0) {
+          lds[o[u]] = v[u].x;
+          lds[o[u] + 1] = v[u].y;
+          lds[o[u] + 2] = v[u].z;
+          lds[o[u] + 3] = v[u].w;
+        }
+    }
+    return;
+  }
+  const int SR = 256 / W, rl0 = tid / W, col = tid - rl0 * W;
+  if (rl0 >= SR) return;
+  for (int row0 = rl0; row0 < nrows; row0 += 8 * SR) {
+    float v[8];
+    int o[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int row = row0 + u * SR;
+      const float* p = row < nrows ? src(row) : nullptr;
+      v[u] = p ? p[col] : 0.f;
+      o[u] = row < nrows ? dst(row) + col : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (o[u] >= 0) lds[o[u]] = v[u];
+  }
+}
+
+// row / R for row < 2^16 through the float reciprocal, corrected to exact
+__device__ __forceinline__ int div_small(int row, int R, float invR) {
+  int c = (int)((float)row * invR);
+  c += (row - c * R >= R) ? 1 : ((row - c * R < 0) ? -1 : 0);
+  return c;
+}
 __host__ __device__ inline int tm_ps(int rows, int Wp) {  // plane stride (floats), = 16 mod 32
   const int f = rows * Wp;
   return f + ((16 - f % 32) + 32) % 32;
@@ -257,10 +314,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3m_kernel(Conv3Args a) {
     const unsigned off = k < K ? (unsigned)(c * PS + (t / 3) * Wp + (t % 3) * d) : 0u;
     koff[s >> 1] |= off << (16 * (s & 1));
   }
-  // staging: thread = (row lane rl, column col) copies column col of staged rows
-  // rl, rl + SR, ...; the d halo columns of every row are zeroed once here and
+  // staging (stage_rows): the d halo columns of every row are zeroed once here and
   // never written again (every tile stages the longest band's R rows)
-  const int R = a.g.TH + 2, SR = 256 / a.W, rl0 = tid / a.W, col0 = tid - rl0 * a.W;
+  const int R = a.g.TH + 2;
+  const float invR = 1.0f / (float)R;
   for (int i = tid; i < C * R * 2 * d; i += 256) {
     const int row = i / (2 * d), e = i - row * (2 * d);
     const int c = row / R, rr = row - c * R;
@@ -271,29 +328,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3m_kernel(Conv3Args a) {
     int r, k0, th;
     band_of(a.g, a.H, tile - b * a.g.nband, r, k0, th);
     __syncthreads();  // previous tile's readers done
-    if (rl0 < SR) {
-      // 8 loads in flight per thread (a serial load-store walk waits out the HBM
-      // latency on every row)
-      const float* xb = a.x + (size_t)b * C * a.H * a.W + col0;
-      const float invR = 1.0f / (float)R;
-      for (int row0 = rl0; row0 < C * R; row0 += 8 * SR) {
-        float v[8];
-        int dst[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int row = row0 + u * SR;
-          int c = (int)((float)row * invR);  // exact: row < 2^16 (host-checked C R < 65536)
-          c += (row - c * R >= R) ? 1 : ((row - c * R < 0) ? -1 : 0);
-          const int rr = row - c * R;
-          const int h = r + (k0 - 1 + rr) * d;
-          const bool ok = row < C * R && h >= 0 && h < a.H;
-          v[u] = ok ? xb[((size_t)c * a.H + h) * a.W] : 0.f;
-          dst[u] = row < C * R ? c * PS + rr * Wp + d + col0 : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (dst[u] >= 0) xl[dst[u]] = v[u];
-      }
+    {
+      const float* xb = a.x + (size_t)b * C * a.H * a.W;
+      const int H = a.H, W = a.W, hr = r + (k0 - 1) * d;
+      // staged row = (channel c, band row rr): image row hr + rr d (zeros outside)
+      stage_rows(
+          xl, C * R, W,
+          [&](int row) -> const float* {
+            const int c = div_small(row, R, invR), h = hr + (row - c * R) * d;
+            return h >= 0 && h < H ? xb + ((size_t)c * H + h) * W : nullptr;
+          },
+          [&](int row) {
+            const int c = div_small(row, R, invR);
+            return c * PS + (row - c * R) * Wp + d;
+          });
     }
     __syncthreads();
     const int npx = th * a.W, nmt = (npx + 15) >> 4;
@@ -479,7 +527,8 @@ __global__ __launch_bounds__(512) void wgrad3x3_kernel(WgradArgs a) {
 // partials are summed in LDS in wave order and each workgroup writes one partial
 // dW, which wsum_kernel adds in a fixed order (deterministic, no atomics).
 // ---------------------------------------------------------------------------- //
-constexpr int TW_XL = 36 * 1024, TW_DL = 28 * 1024;  // staged x / dy bytes per workgroup
+// staged x / dy bytes per workgroup (2 workgroups per CU; 3 would spill the accumulators)
+constexpr int TW_XL = 36 * 1024, TW_DL = 28 * 1024;
 
 template <int C>
 __global__ __launch_bounds__(256, 2) void wgrad3x3m_kernel(WgradArgs a) {
@@ -510,50 +559,37 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3m_kernel(WgradArgs a) {
     const int c = row / R, rr = row - c * R;
     xl[c * PS + rr * Wp + (e < d ? e : a.W + e)] = 0.f;
   }
-  const int SR = 256 / a.W, rl0 = tid / a.W, col0 = tid - rl0 * a.W;
-  const float invR = 1.0f / (float)R, invT = 1.0f / (float)TH;
+  const float invR = 1.0f / (float)R, invT = 1.0f / (float)TH, invW = 1.0f / (float)a.W;
   for (int tile = blockIdx.x; tile < a.B * a.g.nband; tile += gridDim.x) {
     const int b = tile / a.g.nband;
     int r, k0, th;
     band_of(a.g, a.H, tile - b * a.g.nband, r, k0, th);
     __syncthreads();  // previous tile's readers done
-    if (rl0 < SR) {
-      const float* xb = a.x + (size_t)b * C * a.H * a.W + col0;
-      for (int row0 = rl0; row0 < C * R; row0 += 8 * SR) {  // 8 loads in flight per thread
-        float v[8];
-        int dst[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int row = row0 + u * SR;
-          int c = (int)((float)row * invR);  // exact after the +-1 fix-up: row < 2^16 (host-checked)
-          c += (row - c * R >= R) ? 1 : ((row - c * R < 0) ? -1 : 0);
-          const int rr = row - c * R;
-          const int h = r + (k0 - 1 + rr) * d;
-          v[u] = (row < C * R && h >= 0 && h < a.H) ? xb[((size_t)c * a.H + h) * a.W] : 0.f;
-          dst[u] = row < C * R ? c * PS + rr * Wp + d + col0 : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (dst[u] >= 0) xl[dst[u]] = v[u];
-      }
-      const float* db = a.dy + (size_t)b * C * a.H * a.W + col0;
-      for (int row0 = rl0; row0 < C * TH; row0 += 8 * SR) {
-        float v[8];
-        int dst[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int row = row0 + u * SR;
-          int o = (int)((float)row * invT);
-          o += (row - o * TH >= TH) ? 1 : ((row - o * TH < 0) ? -1 : 0);
-          const int jr = row - o * TH;
-          const int h = r + (k0 + jr) * d;
-          v[u] = (row < C * TH && jr < th) ? db[((size_t)o * a.H + h) * a.W] : 0.f;
-          dst[u] = row < C * TH ? o * DS + jr * a.W + col0 : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (dst[u] >= 0) dl[dst[u]] = v[u];
-      }
+    {
+      // one pass over the C R x rows (channel c, band row rr: image row hr + rr d)
+      // and then the C TH dy rows (channel o, band row jr < th), so the x tail's
+      // loads overlap the first dy loads
+      const float* xb = a.x + (size_t)b * C * a.H * a.W;
+      const float* db = a.dy + (size_t)b * C * a.H * a.W;
+      const int H = a.H, W = a.W, hr = r + (k0 - 1) * d, NX = C * R;
+      stage_rows(
+          lds, NX + C * TH, W,
+          [&](int row) -> const float* {
+            if (row < NX) {
+              const int c = div_small(row, R, invR), h = hr + (row - c * R) * d;
+              return h >= 0 && h < H ? xb + ((size_t)c * H + h) * W : nullptr;
+            }
+            const int o = div_small(row - NX, TH, invT), jr = row - NX - o * TH;
+            return jr < th ? db + ((size_t)o * H + r + (k0 + jr) * d) * W : nullptr;
+          },
+          [&](int row) {
+            if (row < NX) {
+              const int c = div_small(row, R, invR);
+              return c * PS + (row - c * R) * Wp + d;
+            }
+            const int o = div_small(row - NX, TH, invT);
+            return TW_XL / 4 + o * DS + (row - NX - o * TH) * W;
+          });
     }
     __syncthreads();
     const int npx = th * a.W, nks = (npx + 3) >> 2;
@@ -561,7 +597,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3m_kernel(WgradArgs a) {
       const int p = 4 * s + kk;
       const bool pv = p < npx;  // k beyond the band: A = 0 (B reads pixel 0, finite)
       const int pp = pv ? p : 0;
-      const int row = pp / a.W, col = pp - row * a.W;
+      const int row = div_small(pp, a.W, invW), col = pp - row * a.W;
       const float* xp = xl + row * Wp + col;
       float av[NO], bv[NJ];
 #pragma unroll
@@ -860,6 +896,142 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__
   gh[i] = h[i] <= 0.f ? 0.f : g;
 }
 
+// ---------------------------------------------------------------------------- //
+// The res stem in training (model.py:104-110): y = AvgPool2d(ph, pw)(relu(conv0(x)))
+// (no pool: ph = pw = 1), conv0 = Conv2d(1, C, 3, padding 1, no bias), and its
+// weight gradient (the input needs none).  One workgroup per clip at a time: the
+// clip's [H][W] map is staged into LDS with a zero border; thread (o, q) owns output
+// channel o (its 9 weights in registers) and every Q-th output pixel.  The pool sums
+// its window in row-major order and divides, as avg_pool2d's kernels do.  Backward
+// recomputes the conv (9 FMAs) for the ReLU mask instead of keeping the pre-pool map;
+// each thread accumulates its channel's 9 weight gradients, summed over the Q
+// threads of a channel in a fixed order into one partial per workgroup (wsum_kernel).
+// ---------------------------------------------------------------------------- //
+constexpr int STEM_XL = 8192;  // floats of the staged (H+2) x (W+2) map
+
+struct StemArgs {
+  const float* x;   // [B][H][W]
+  const float* w;   // [C][1][3][3]
+  const float* gy;  // backward: [B][C][Hp][Wp]
+  float* y;         // forward: [B][C][Hp][Wp]
+  float* part;      // backward: [gridDim.x][C][9]
+  int B, C, H, W, ph, pw;
+};
+
+__device__ __forceinline__ float stem_conv(const float* xs, int Ws, int h, int w, const float (&wr)[9]) {
+  float acc = 0.f;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc = fmaf(wr[t], xs[(h + t / 3) * Ws + w + t % 3], acc);
+  return acc;
+}
+
+// the clip's map into the bordered LDS image, 8 loads in flight per thread (float4s
+// when rows are whole float4s)
+__device__ __forceinline__ void stem_stage(float* xs, const float* xb, int H, int W) {
+  const int Ws = W + 2;
+  if ((W & 3) == 0) {
+    const int n4 = H * W / 4;
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 8 * 256) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 256;
+        v[u] = i < n4 ? *(const float4*)(xb + 4 * i) : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 256;
+        if (i < n4) {
+          const int h = 4 * i / W, w = 4 * i - h * W;
+          float* d = xs + (h + 1) * Ws + w + 1;
+          d[0] = v[u].x; d[1] = v[u].y; d[2] = v[u].z; d[3] = v[u].w;
+        }
+      }
+    }
+    return;
+  }
+  for (int i0 = threadIdx.x; i0 < H * W; i0 += 8 * 256) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 256;
+      v[u] = i < H * W ? xb[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 256;
+      if (i < H * W) {
+        const int h = i / W, w = i - h * W;
+        xs[(h + 1) * Ws + w + 1] = v[u];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void stem_border(float* xs, int H, int W) {
+  const int Ws = W + 2;
+  for (int i = threadIdx.x; i < (H + 2) * Ws; i += 256) {
+    const int h = i / Ws, w = i - h * Ws;
+    if (h == 0 || h == H + 1 || w == 0 || w == W + 1) xs[i] = 0.f;
+  }
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
+  __shared__ float xs[STEM_XL];
+  __shared__ float red[256 * 9];
+  const int Q = 256 / a.C, o = threadIdx.x / Q, q = threadIdx.x - o * Q;
+  const bool act = o < a.C;
+  float wr[9], dw[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wr[t] = act ? a.w[o * 9 + t] : 0.f;
+    dw[t] = 0.f;
+  }
+  const int Ws = a.W + 2, Hp = a.H / a.ph, Wq = a.W / a.pw, np = a.ph * a.pw;
+  stem_border(xs, a.H, a.W);
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    __syncthreads();  // previous clip's readers done (and the border written)
+    stem_stage(xs, a.x + (size_t)b * a.H * a.W, a.H, a.W);
+    __syncthreads();
+    if (!act) continue;
+    const size_t ob = ((size_t)b * a.C + o) * Hp * Wq;
+    if (!BWD) {
+      for (int px = q; px < Hp * Wq; px += Q) {
+        const int i = px / Wq, j = px - i * Wq;
+        float s = 0.f;
+        for (int u = 0; u < a.ph; ++u)
+          for (int v = 0; v < a.pw; ++v) s += fmaxf(stem_conv(xs, Ws, i * a.ph + u, j * a.pw + v, wr), 0.f);
+        a.y[ob + px] = np == 1 ? s : s / (float)np;
+      }
+    } else {
+      for (int px = q; px < a.H * a.W; px += Q) {
+        const int h = px / a.W, w = px - h * a.W, i = h / a.ph, j = w / a.pw;
+        if (i >= Hp || j >= Wq) continue;              // rows / columns the floor pooling drops
+        if (stem_conv(xs, Ws, h, w, wr) <= 0.f) continue;  // ReLU's backward
+        const float g0 = a.gy[ob + i * Wq + j];
+        const float g = np == 1 ? g0 : g0 / (float)np;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) dw[t] = fmaf(g, xs[(h + t / 3) * Ws + w + t % 3], dw[t]);
+      }
+    }
+  }
+  if (!BWD) return;
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 9; ++t) red[threadIdx.x * 9 + t] = dw[t];
+  __syncthreads();
+  if (act && q == 0) {
+    float* pb = a.part + (size_t)blockIdx.x * a.C * 9 + o * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float s = 0.f;
+      for (int k = 0; k < Q; ++k) s += red[(threadIdx.x + k) * 9 + t];
+      pb[t] = s;
+    }
+  }
+}
+
 static int bn_slices(int B, int C) {
   int S = (4 * 256 + C - 1) / C;  // ~4 workgroups per CU in total
   if (S > B) S = B;
@@ -936,7 +1108,7 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   const char* ke = getenv("HONK_TRAIN_CONV");
   if (c == 19 && !(ke && ke[0] == 'v') && train::tm_rows(c, h, w_, dil) > 0) {
     a.g = train::class_bands(h, dil, train::tm_rows(c, h, w_, dil));
-    const int gm = (int)std::min<int64_t>((int64_t)a.B * a.g.nband, 2 * (int64_t)cu_count());
+    const int gm = train::tc_grid((int64_t)a.B * a.g.nband);
     hipLaunchKernelGGL((train::conv3x3m_kernel<19>), dim3(gm), dim3(256), 0, st, a);
   } else if (c == 19) {
     if (np <= 1) hipLaunchKernelGGL((train::conv3x3_kernel<19, 1>), dim3(grid), dim3(256), 0, st, a);
@@ -974,11 +1146,12 @@ WgradPlan wgrad_plan(int64_t batch, int c, int h, int w_, int dil) {
 extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil) {
   if (batch < 1 || (c != 19 && c != 45) || h < 1 || w_ < 1 || dil < 1 || dil > 64) return 0;
   if (train::tc_rows(c, h, w_, dil) < 1) return 0;
-  // either kernel's grid (the environment may switch kernels between this query and the call)
-  const int64_t t0 = batch * train::class_bands(h, dil, train::tc_rows(c, h, w_, dil)).nband;
+  // the largest grid of any kernel choice (the environment may switch kernels between
+  // this query and the call)
+  int64_t t = batch * train::class_bands(h, dil, train::tc_rows(c, h, w_, dil)).nband;
   const int tw = c == 19 ? train::tw_rows(c, h, w_, dil) : 0;
-  const int64_t t1 = tw > 0 ? batch * train::class_bands(h, dil, tw).nband : 0;
-  return (size_t)train::tc_grid(t0 > t1 ? t0 : t1) * c * c * 9 * sizeof(float);
+  if (tw > 0) t = std::max<int64_t>(t, batch * train::class_bands(h, dil, tw).nband);
+  return (size_t)train::tc_grid(t) * c * c * 9 * sizeof(float);
 }
 
 extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
@@ -1109,5 +1282,58 @@ extern "C" int honk_res_tail_bwd_f32(const float* gy, const float* gs, const flo
   hipLaunchKernelGGL(train::tail_bwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
                      (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
   HONK_LAUNCH_CHECK("tail_bwd_kernel");
+  return HONK_OK;
+}
+
+namespace {
+int stem_check(const void* x, const void* w, const void* y, int64_t batch, int32_t c, int32_t h, int32_t w_,
+               int32_t ph, int32_t pw) {
+  if (!x || !w || !y) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 0 || batch > 0x7fffffff || h < 1 || w_ < 1 || ph < 1 || pw < 1 || ph > h || pw > w_)
+    return fail(HONK_ERR_ARG, "bad stem shape (B=%lld H=%d W=%d pool %dx%d)", (long long)batch, h, w_, ph, pw);
+  if (c < 1 || c > 64) return fail(HONK_ERR_UNSUPPORTED, "stem: %d feature maps (1..64)", c);
+  if ((h + 2) * (w_ + 2) > train::STEM_XL) return fail(HONK_ERR_UNSUPPORTED, "stem: %dx%d input too large", h, w_);
+  return HONK_OK;
+}
+int stem_grid(int64_t batch) { return (int)std::min<int64_t>(batch, 3 * (int64_t)cu_count()); }
+}  // namespace
+
+extern "C" int honk_res_stem_fwd_f32(const float* x, const float* w0, float* y, int64_t batch, int32_t c, int32_t h,
+                                     int32_t w_, int32_t ph, int32_t pw, void* stream) {
+  int rc = stem_check(x, w0, y, batch, c, h, w_, ph, pw);
+  if (rc) return rc;
+  if (batch == 0) return HONK_OK;
+  train::StemArgs a{x, w0, nullptr, y, nullptr, (int)batch, c, h, w_, ph, pw};
+  hipLaunchKernelGGL(train::stem_kernel<false>, dim3(stem_grid(batch)), dim3(256), 0, (hipStream_t)stream, a);
+  HONK_LAUNCH_CHECK("stem_kernel");
+  return HONK_OK;
+}
+
+extern "C" size_t honk_res_stem_wgrad_workspace_bytes(int64_t batch, int32_t c) {
+  if (batch < 1 || c < 1 || c > 64) return 0;
+  return (size_t)stem_grid(batch) * c * 9 * sizeof(float);
+}
+
+extern "C" int honk_res_stem_wgrad_f32(const float* x, const float* w0, const float* gy, float* dw, int64_t batch,
+                                       int32_t c, int32_t h, int32_t w_, int32_t ph, int32_t pw, void* workspace,
+                                       size_t ws_bytes, void* stream) {
+  int rc = stem_check(x, w0, dw, batch, c, h, w_, ph, pw);
+  if (rc) return rc;
+  if (!gy) return fail(HONK_ERR_ARG, "null pointer argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (batch == 0) {
+    HONK_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)c * 9 * sizeof(float), st));
+    return HONK_OK;
+  }
+  const size_t need = honk_res_stem_wgrad_workspace_bytes(batch, c);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  const int grid = stem_grid(batch);
+  train::StemArgs a{x, w0, gy, nullptr, (float*)workspace, (int)batch, c, h, w_, ph, pw};
+  hipLaunchKernelGGL(train::stem_kernel<true>, dim3(grid), dim3(256), 0, st, a);
+  HONK_LAUNCH_CHECK("stem_kernel");
+  const int n = c * 9;
+  hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, 64)), dim3(256), 0, st, (const float*)workspace, dw,
+                     n, grid);
+  HONK_LAUNCH_CHECK("wsum_kernel");
   return HONK_OK;
 }

@@ -153,15 +153,20 @@ class SpeechResModel(SerializableModule):
         self.honk_native_train = True
 
     # -- reference forward (CPU tensors / training mode): model.py:104-121 --
-    # native_convs: training on a ROCm tensor runs the block convs (conv1..convN)
-    # on honk_conv3x3_f32 / honk_conv3x3_wgrad_f32 where they cover the shape
-    # (any dilation, 19 or 45 maps) and the train-mode BatchNorms on honk_bn_train_*
-    # (honk_amd/conv3x3.py); ReLU, residual, conv0, pool, mean, Linear and the loss
-    # stay PyTorch autograd
+    # native_convs: training on a ROCm tensor runs the stem (conv0 + relu + pool) on
+    # honk_res_stem_*, the block convs (conv1..convN) on honk_conv3x3_f32 /
+    # honk_conv3x3_wgrad_f32 where they cover the shape (any dilation, 19 or 45 maps)
+    # and each block's relu / residual / train-mode BatchNorm on honk_res_tail_*
+    # (honk_amd/conv3x3.py); the mean, Linear and the loss stay PyTorch autograd
     def _torch_forward(self, x, native_convs=False):
-        x = x.unsqueeze(1)
+        x_in, x = x, x.unsqueeze(1)
         for i in range(self.n_layers + 1):
             conv = getattr(self, "conv{}".format(i))
+            pool = getattr(self, "pool", None)
+            if native_convs and i == 0 and _conv3x3.stem_supported(x_in, conv, pool):
+                # conv0, relu and the avg-pool as one native stem
+                x = old_x = _conv3x3.stem(x_in, conv, pool)
+                continue
             if native_convs and i > 0 and _conv3x3.supported(x, conv) and \
                     _conv3x3.bn_supported(x, getattr(self, "bn{}".format(i))):
                 # conv, then relu / residual add / train BatchNorm as one fused tail

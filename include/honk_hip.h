@@ -199,6 +199,21 @@ int honk_res_tail_fwd_f32(const float* h, const float* old, float* s, float* y, 
 int honk_res_tail_bwd_f32(const float* gy, const float* gs, const float* y, const float* invstd, const float* h,
                           float* gh, float* gold, int64_t batch, int32_t c, int64_t hw, void* workspace,
                           size_t workspace_bytes, void* stream);
+/*
+ * The res stem in training (model.py:104-110 in training: y = relu(conv0(x)), then
+ * AvgPool2d((ph, pw)) when the config has res_pool; ph = pw = 1 without pool),
+ * replacing the conv0 / relu / avg_pool2d kernels autograd runs and their backward
+ * (utils/train.py:131-134).  x [B][H][W] fp32 (the MFCC input, no gradient), w0 the
+ * [C][1][3][3] conv0 weight, y / gy [B][C][H/ph][W/pw]; 1 <= C <= 64, (H+2)(W+2) <= 8192.
+ * honk_res_stem_wgrad_f32: dw0 = d(sum gy * y)/d w0 (the ReLU mask recomputed from x),
+ * deterministic (per-workgroup partials summed in a fixed order).
+ */
+int honk_res_stem_fwd_f32(const float* x, const float* w0, float* y, int64_t batch, int32_t c, int32_t h, int32_t w_,
+                          int32_t ph, int32_t pw, void* stream);
+size_t honk_res_stem_wgrad_workspace_bytes(int64_t batch, int32_t c);
+int honk_res_stem_wgrad_f32(const float* x, const float* w0, const float* gy, float* dw0, int64_t batch, int32_t c,
+                            int32_t h, int32_t w_, int32_t ph, int32_t pw, void* workspace, size_t workspace_bytes,
+                            void* stream);
 
 /* ---- diagnostics --------------------------------------------------------------- */
 const char* honk_last_error(void);

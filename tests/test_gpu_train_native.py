@@ -189,3 +189,30 @@ def test_res_tail_bitwise_vs_unfused(B, C, H, W, res, keep):
     assert len(a) == len(b)
     for i, (u, v) in enumerate(zip(a, b)):
         assert torch.equal(u, v), (i, float((u.double() - v.double()).abs().max()))
+
+
+@pytest.mark.parametrize("B,C,H,W,pool", [(64, 19, 101, 40, (2, 2)), (5, 45, 101, 40, (4, 3)),
+                                          (3, 19, 101, 40, None), (2, 45, 101, 40, None), (3, 19, 9, 7, (2, 3))])
+def test_res_stem_matches_float64(B, C, H, W, pool):
+    """honk_res_stem_fwd_f32 / wgrad_f32 (conv0 + relu [+ AvgPool2d], model.py:104-110)
+    vs the same ops in float64 on the CPU: output within 1e-6 and the conv0 weight
+    gradient within 1e-5 of their max |value| (fp32 sums over 9 taps / B*H*W pixels)."""
+    g = torch.Generator(device=DEV).manual_seed(B + C + H + W)
+    x = torch.randn(B, H, W, device=DEV, generator=g)
+    conv0 = torch.nn.Conv2d(1, C, (3, 3), padding=(1, 1), bias=False).to(DEV)
+    pm = torch.nn.AvgPool2d(pool) if pool else None
+    assert hc.stem_supported(x, conv0, pm)
+    y = hc.stem(x, conv0, pm)
+    gy = torch.randn(y.shape, device=DEV, generator=g)
+    (dw,) = torch.autograd.grad(y, conv0.weight, gy)
+    x64 = x.double().cpu().unsqueeze(1)
+    w64 = conv0.weight.detach().double().cpu().requires_grad_(True)
+    r = F.relu(F.conv2d(x64, w64, padding=1))
+    if pool:
+        r = F.avg_pool2d(r, pool)
+    (dw64,) = torch.autograd.grad(r, w64, gy.double().cpu())
+    assert y.shape == r.shape
+    assert _rel(y, r) < 1e-6
+    assert _rel(dw, dw64) < 1e-5
+    (dw2,) = torch.autograd.grad(hc.stem(x, conv0, pm), conv0.weight, gy)
+    assert torch.equal(dw, dw2)  # deterministic
