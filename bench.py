@@ -476,9 +476,10 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
                      "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
                      "flop_per_clip": fl,
                      "flop_def": "2 x (forward + input-grad + weight-grad MACs), conv0 has no input grad"},
-        "note": "native kernels: the block convs' forward / input grad / weight grad, train-mode BatchNorm "
-                "fwd/bwd, fused SGD over the flat all-reduced bucket; conv0, pooling, ReLU, residual, mean, "
-                "Linear and the loss run on PyTorch autograd on the device"}
+        "note": "native kernels: the stem (conv0 + relu + avg-pool, conv0 weight grad), the block convs' "
+                "forward / input grad / weight grad on fp32 MFMA, each block's relu + residual + train-mode "
+                "BatchNorm fwd/bwd fused, fused SGD over the flat all-reduced bucket; the mean, Linear and the "
+                "loss run on PyTorch autograd on the device"}
 
 
 def rank_main(args):

@@ -6,10 +6,11 @@ res8/res26 and -narrow, d = 2**(i//3) for res15 and res15-narrow) as an autograd
 function whose forward, input gradient and weight gradient are
 ``honk_conv3x3_f32`` / ``honk_conv3x3_wgrad_f32``;
 ``batch_norm_train(x, bn)`` is the blocks' train-mode ``BatchNorm2d(affine=False)``
-(model.py:100, 117-118) on ``honk_bn_train_fwd/bwd_f32``.  The rest of the
-training graph (ReLU, residual, conv0, pooling, mean, Linear, loss) stays PyTorch
-autograd on the device, so ``utils/train.py``'s loop (train.py:131-134) runs
-unchanged.
+(model.py:100, 117-118) on ``honk_bn_train_fwd/bwd_f32``; ``res_tail`` fuses a
+block's relu, residual add and that BatchNorm (``honk_res_tail_fwd/bwd_f32``) and
+``stem`` is conv0 + relu + avg-pool (``honk_res_stem_*``, model.py:104-110).  The
+mean, Linear and loss stay PyTorch autograd on the device, so ``utils/train.py``'s
+loop (train.py:131-134) runs unchanged.
 """
 from __future__ import annotations
 

@@ -372,6 +372,152 @@ __global__ __launch_bounds__(256, 2) void conv3x3m_kernel(Conv3Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------- //
+// conv3x3d_kernel<C> (C <= 20, d <= 4, W a multiple of 4): conv3x3m_kernel's MFMA
+// loop (same k order, bit-identical) on a double-buffered tile staged by LDS-DMA
+// (buffer_load ... lds, 16 B per lane): while the 8 waves multiply tile t out of one
+// buffer, the DMA fills the other with tile t + grid, so HBM latency never stalls
+// the MFMAs.  An LDS row is [4 zeros | W pixels | 4 zeros] (TD_PAD = 4 >= d), a
+// plane R rows at a stride = 16 mod 32 floats, every 16-B chunk either an HBM chunk
+// of the clip or an out-of-range buffer offset (the bounds check returns zeros:
+// the halo columns, rows outside the image and plane padding).  One workgroup of
+// 512 threads per CU (two 60-KB buffers).
+// ---------------------------------------------------------------------------- //
+constexpr int TD_PAD = 4;           // zero floats left / right of every staged row
+constexpr int TD_BUF = 64 * 1024;   // bytes per buffer (two per workgroup)
+constexpr int TD_ITER = 8;          // DMA instructions per wave per tile (8 waves x 8 x 1 KB)
+
+__device__ __forceinline__ void td_wait_vm0() { __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8)); }
+
+struct TdGeo {
+  int Wr, PS, R, nchunk;  // padded row floats, plane stride, rows per plane, chunks per buffer (mult. of 64)
+};
+__host__ __device__ inline TdGeo td_geo(int C, int W, int TH) {
+  TdGeo g;
+  g.Wr = W + 2 * TD_PAD;
+  g.R = TH + 2;
+  const int f = g.R * g.Wr;
+  g.PS = f + ((16 - f % 32) + 32) % 32;  // a multiple of 4 (Wr is): whole chunks
+  g.nchunk = (C * g.PS / 4 + 63) / 64 * 64;
+  return g;
+}
+
+template <int C>
+__global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
+  static_assert(C <= 20, "conv3x3d_kernel: C <= 20");
+  constexpr int K = 9 * C, KS = (K + 3) / 4;
+  __shared__ __attribute__((aligned(16))) float tdl[2 * TD_BUF / 4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int d = a.g.d, W = a.W, H = a.H;
+  const TdGeo G = td_geo(C, W, a.g.TH);
+  float wr[KS][2];
+  unsigned koff[(KS + 1) / 2];
+#pragma unroll
+  for (int s = 0; s < (KS + 1) / 2; ++s) koff[s] = 0;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + kk, c = k / 9, t = k - 9 * c;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int o = 16 * n + i16;
+      float v = 0.f;
+      if (o < C && k < K) v = a.flip ? a.w[(c * C + o) * 9 + 8 - t] : a.w[(o * C + c) * 9 + t];
+      wr[s][n] = v;
+    }
+    const unsigned off = k < K ? (unsigned)(c * G.PS + (t / 3) * G.Wr + (t % 3) * d) : 0u;
+    koff[s >> 1] |= off << (16 * (s & 1));
+  }
+  // per lane and DMA instruction i: chunk e = (wave TD_ITER + i) 64 + lane of the
+  // buffer -> (plane c, row rr, 16-B column cc); tile-invariant byte offset of the
+  // chunk in its clip (row 0), or -1 for a zero chunk
+  int cbase[TD_ITER], crow[TD_ITER];
+#pragma unroll
+  for (int i = 0; i < TD_ITER; ++i) {
+    const int e = (wave * TD_ITER + i) * 64 + lane;
+    const int c = e * 4 / G.PS, rem = e * 4 - c * G.PS, rr = rem / G.Wr, col = rem - rr * G.Wr - TD_PAD;
+    const bool ok = e < G.nchunk && c < C && rr < G.R && col >= 0 && col < W;
+    cbase[i] = ok ? (c * H * W + col) * 4 : -1;
+    crow[i] = rr;
+  }
+  const int ntile = a.B * a.g.nband;
+  const size_t clip = (size_t)C * H * W;
+  auto issue = [&](int tile, float* buf) {
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (size_t)b * clip), (short)0, (int)(clip * 4), 0x00020000);
+    const int hr = r + (k0 - 1) * d;
+#pragma unroll
+    for (int i = 0; i < TD_ITER; ++i) {
+      const int h = hr + crow[i] * d;
+      const unsigned voff =
+          (cbase[i] >= 0 && h >= 0 && h < H) ? (unsigned)(cbase[i] + h * W * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TD_ITER + i) * 256)),
+          16, voff, 0, 0, 0);
+    }
+  };
+  float* buf0 = tdl;
+  float* buf1 = tdl + TD_BUF / 4;
+  if ((int)blockIdx.x < ntile) issue(blockIdx.x, buf0);
+  int it = 0;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x, ++it) {
+    float* cur = (it & 1) ? buf1 : buf0;
+    float* nxt = (it & 1) ? buf0 : buf1;
+    td_wait_vm0();
+    __syncthreads();  // this tile's DMA landed everywhere; nobody reads nxt any more
+    if (tile + (int)gridDim.x < ntile) issue(tile + gridDim.x, nxt);
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
+    const int npx = th * W, nmt = (npx + 15) >> 4;
+    float* yb = a.y + (size_t)b * clip;
+    for (int m = wave; m < nmt; m += 8) {
+      const int p = 16 * m + i16;
+      const bool pv = p < npx;
+      const int j = pv ? p / W : 0, col = pv ? p - j * W : 0;
+      const float* xp = cur + j * G.Wr + col + TD_PAD - d;
+      f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float xv = xp[(koff[s >> 1] >> (16 * (s & 1))) & 0xffffu];
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s][0], xv, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s][1], xv, acc[1], 0, 0, 0);
+      }
+      if (pv) {
+        const size_t pix = (size_t)(r + (k0 + j) * d) * W + col;
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int o = 16 * n + 4 * kk + i;
+            if (o < C) yb[(size_t)o * H * W + pix] = acc[n][i];
+          }
+      }
+    }
+  }
+  td_wait_vm0();  // no DMA left in flight when the workgroup retires
+}
+
+// class rows per conv3x3d_kernel tile (0: not applicable): the largest band whose
+// buffer fits TD_BUF with TD_ITER DMA instructions per wave, balanced over the class
+static int td_rows(int C, int H, int W, int d) {
+  if (d > TD_PAD || (W & 3) || W > 256 || C > 20) return 0;
+  const int hc = (H + d - 1) / d;
+  int th = 0;
+  for (int t = 1; t <= hc; ++t) {
+    const TdGeo g = td_geo(C, W, t);
+    if (g.nchunk * 16 > TD_BUF || g.nchunk > 8 * TD_ITER * 64 || C * g.PS >= 65536) break;
+    th = t;
+  }
+  if (th < 1) return 0;
+  const int nb = (hc + th - 1) / th;
+  return (hc + nb - 1) / nb;
+}
+
 // class rows per conv3x3m_kernel tile: C planes of (TH + 2) x (W + 2d) (+ pad) in TM_XL
 static int tm_rows(int C, int H, int W, int d) {
   const int Wp = W + 2 * d;
@@ -633,6 +779,171 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3m_kernel(WgradArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------- //
+// wgrad3x3d_kernel<C> (C <= 20, d <= 4, W a multiple of 4): wgrad3x3m_kernel's GEMM
+// on conv3x3d_kernel's double-buffered LDS-DMA staging.  A buffer holds the x band
+// (TdGeo planes) followed by the dy band ([o][TH W] at a plane stride = 4 mod 64, so
+// the 16 A lanes of a read hit 16 banks); 8 waves take interleaved k-steps; their
+// partials are summed in wave order, one partial per workgroup (wsum_kernel).
+// ---------------------------------------------------------------------------- //
+__host__ __device__ inline int twd_ds(int TH, int W) {  // dy plane stride (floats)
+  const int f = TH * W;
+  return f + ((4 - f % 64) + 64) % 64;
+}
+__host__ __device__ inline int twd_nchunk(int C, int W, int TH) {
+  const TdGeo g = td_geo(C, W, TH);
+  return (C * g.PS / 4 + C * twd_ds(TH, W) / 4 + 63) / 64 * 64;
+}
+
+template <int C>
+__global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
+  static_assert(C <= 20, "wgrad3x3d_kernel: C <= 20");
+  constexpr int K9 = 9 * C, NJ = (K9 + 15) / 16, NO = (C + 15) / 16;
+  __shared__ __attribute__((aligned(16))) float tdl[2 * TD_BUF / 4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int d = a.g.d, W = a.W, H = a.H, TH = a.g.TH;
+  const TdGeo G = td_geo(C, W, TH);
+  const int DS = twd_ds(TH, W), XF = C * G.PS;  // dy planes start at float XF
+  const int nch = twd_nchunk(C, W, TH);
+  int joff[NJ];
+#pragma unroll
+  for (int n = 0; n < NJ; ++n) {
+    const int j = 16 * n + i16, ci = j / 9, t = j - 9 * ci;
+    joff[n] = j < K9 ? ci * G.PS + (t / 3) * G.Wr + (t % 3) * d : 0;
+  }
+  f32x4_t acc[NO][NJ];
+#pragma unroll
+  for (int m = 0; m < NO; ++m)
+#pragma unroll
+    for (int n = 0; n < NJ; ++n) acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // per lane and DMA instruction i: chunk e -> x chunk (plane c, row rr: image row
+  // hr + rr d) or dy chunk (plane o, band row jr: image row r + (k0 + jr) d), as the
+  // byte offset in its clip tensor at row 0 and the band row; kind 0 = zero chunk
+  int cbase[TD_ITER], crow[TD_ITER], ckind[TD_ITER];
+#pragma unroll
+  for (int i = 0; i < TD_ITER; ++i) {
+    const int e = (wave * TD_ITER + i) * 64 + lane, f = e * 4;
+    cbase[i] = 0;
+    crow[i] = 0;
+    ckind[i] = 0;
+    if (e < nch && f < XF) {
+      const int c = f / G.PS, rem = f - c * G.PS, rr = rem / G.Wr, col = rem - rr * G.Wr - TD_PAD;
+      if (rr < G.R && col >= 0 && col < W) {
+        cbase[i] = (c * H * W + col) * 4;
+        crow[i] = rr - 1;
+        ckind[i] = 1;
+      }
+    } else if (e < nch && f - XF < C * DS) {
+      const int g = f - XF, o = g / DS, rem = g - o * DS, jr = rem / W, col = rem - jr * W;
+      if (jr < TH) {
+        cbase[i] = (o * H * W + col) * 4;
+        crow[i] = jr;
+        ckind[i] = 2;
+      }
+    }
+  }
+  const int ntile = a.B * a.g.nband;
+  const size_t clip = (size_t)C * H * W;
+  auto issue = [&](int tile, float* buf) {
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (size_t)b * clip), (short)0, (int)(clip * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.dy + (size_t)b * clip), (short)0, (int)(clip * 4), 0x00020000);
+    const int hb = r + k0 * d;
+#pragma unroll
+    for (int i = 0; i < TD_ITER; ++i) {
+      const int h = hb + crow[i] * d;
+      const bool ok = ckind[i] != 0 && h >= 0 && h < H && (ckind[i] == 1 || crow[i] < th);
+      const unsigned voff = ok ? (unsigned)(cbase[i] + h * W * 4) : 0x80000000u;
+      // one LDS slot per lane: a lane's chunk comes from dy (rd) or x / zeros (rx); the
+      // instruction that straddles the x / dy boundary runs twice under complementary
+      // exec masks, every slot written once
+      if (ckind[i] == 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rd, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TD_ITER + i) * 256)),
+            16, voff, 0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rx, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TD_ITER + i) * 256)),
+            16, voff, 0, 0, 0);
+    }
+  };
+  float* buf0 = tdl;
+  float* buf1 = tdl + TD_BUF / 4;
+  if ((int)blockIdx.x < ntile) issue(blockIdx.x, buf0);
+  const float invW = 1.0f / (float)W;
+  int it = 0;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x, ++it) {
+    float* cur = (it & 1) ? buf1 : buf0;
+    float* nxt = (it & 1) ? buf0 : buf1;
+    td_wait_vm0();
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntile) issue(tile + gridDim.x, nxt);
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
+    const int npx = th * W, nks = (npx + 3) >> 2;
+    const float* dl = cur + XF;
+    for (int s = wave; s < nks; s += 8) {
+      const int p = 4 * s + kk;
+      const bool pv = p < npx;
+      const int pp = pv ? p : 0;
+      const int row = div_small(pp, W, invW), col = pp - row * W;
+      const float* xp = cur + row * G.Wr + col + TD_PAD - d;
+      float av[NO], bv[NJ];
+#pragma unroll
+      for (int m = 0; m < NO; ++m) {
+        const int o = 16 * m + i16;
+        av[m] = (pv && o < C) ? dl[o * DS + pp] : 0.f;
+      }
+#pragma unroll
+      for (int n = 0; n < NJ; ++n) bv[n] = xp[joff[n]];
+#pragma unroll
+      for (int m = 0; m < NO; ++m)
+#pragma unroll
+        for (int n = 0; n < NJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+  }
+  td_wait_vm0();
+  float* pb = a.part + (size_t)blockIdx.x * C * K9;
+  constexpr int NJP = NJ * 16;
+#pragma unroll
+  for (int m = 0; m < NO; ++m) {
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < NJ; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tdl[(wave * 16 + 4 * kk + i) * NJP + 16 * n + i16] = acc[m][n][i];
+    __syncthreads();
+    for (int idx = tid; idx < 16 * K9; idx += 512) {
+      const int i = idx / K9, j = idx - i * K9, o = 16 * m + i;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += tdl[(16 * w + i) * NJP + j];
+      if (o < C) pb[o * K9 + j] = v;
+    }
+  }
+}
+
+// class rows per wgrad3x3d_kernel tile (0: not applicable)
+static int twd_rows(int C, int H, int W, int d) {
+  if (d > TD_PAD || (W & 3) || W > 256 || C > 20) return 0;
+  const int hc = (H + d - 1) / d;
+  int th = 0;
+  for (int t = 1; t <= hc; ++t) {
+    if (twd_nchunk(C, W, t) > 8 * TD_ITER * 64 || C * td_geo(C, W, t).PS >= 65536) break;
+    th = t;
+  }
+  if (th < 1) return 0;
+  const int nb = (hc + th - 1) / th;
+  return (hc + nb - 1) / nb;
+}
+
 // class rows per wgrad3x3m_kernel tile: C x planes of (TH + 2) x (W + 2d) in TW_XL,
 // C dy planes of TH x W in TW_DL, the 4 waves' 64 x 16 NJ partial sums in both
 static int tw_rows(int C, int H, int W, int d) {
@@ -647,19 +958,28 @@ static int tw_rows(int C, int H, int W, int d) {
   return (hc + nb - 1) / nb;
 }
 
-// dw[i] = sum over the nblk per-workgroup partials, fixed order: 64 outputs per
-// workgroup, 4 strands over k (k = strand mod 4) combined in LDS
+// dw[i] = sum over the nblk per-workgroup partials, fixed order: 16 outputs per
+// workgroup, 16 strands over k (k = strand mod 16, 8 loads in flight per strand)
+// combined in strand order in LDS
+constexpr int WSUM_OUT = 16;
 __global__ __launch_bounds__(256) void wsum_kernel(const float* __restrict__ part, float* __restrict__ dw, int n,
                                                    int nblk) {
-  __shared__ float red[4][64];
-  const int il = threadIdx.x & 63, strand = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + il;
+  __shared__ float red[16][WSUM_OUT + 1];
+  const int il = threadIdx.x & (WSUM_OUT - 1), strand = threadIdx.x / WSUM_OUT;
+  const int i = blockIdx.x * WSUM_OUT + il;
   float s = 0.f;
-  if (i < n)
-    for (int k = strand; k < nblk; k += 4) s += part[(size_t)k * n + i];
+  if (i < n) {
+#pragma unroll 8
+    for (int k = strand; k < nblk; k += 16) s += part[(size_t)k * n + i];
+  }
   red[strand][il] = s;
   __syncthreads();
-  if (strand == 0 && i < n) dw[i] = (red[0][il] + red[1][il]) + (red[2][il] + red[3][il]);
+  if (strand == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][il];
+    dw[i] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------- //
@@ -1032,6 +1352,96 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
   }
 }
 
+// stem_kernel with the pool window fixed at compile time: a thread item is SW
+// horizontally adjacent pooled outputs (SW = 4 without pool, where each output is
+// one conv pixel), read once as a (PH + 2) x (SW PW + 2) register patch: 16 LDS
+// reads for a 2x2 window instead of 36, and one index computation per item.  Same
+// arithmetic as stem_kernel: the 9-tap fmaf chain per conv pixel, the window summed
+// row-major then divided; backward accumulates each thread's dW in item order.
+template <bool BWD, int PH, int PW, int SW>
+__global__ __launch_bounds__(256) void stem_tile_kernel(StemArgs a) {
+  constexpr int PR = PH + 2, PC = SW * PW + 2, NP = PH * PW;
+  __shared__ float xs[STEM_XL];
+  __shared__ float red[256 * 9];
+  const int Q = 256 / a.C, o = threadIdx.x / Q, q = threadIdx.x - o * Q;
+  const bool act = o < a.C;
+  float wr[9], dw[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wr[t] = act ? a.w[o * 9 + t] : 0.f;
+    dw[t] = 0.f;
+  }
+  const int Ws = a.W + 2, Hp = a.H / PH, Wq = a.W / PW, ipr = Wq / SW;  // host: SW divides Wq
+  const float inv_ipr = 1.0f / (float)ipr;
+  stem_border(xs, a.H, a.W);
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    __syncthreads();
+    stem_stage(xs, a.x + (size_t)b * a.H * a.W, a.H, a.W);
+    __syncthreads();
+    if (!act) continue;
+    const size_t ob = ((size_t)b * a.C + o) * Hp * Wq;
+    for (int it = q; it < Hp * ipr; it += Q) {
+      const int i = div_small(it, ipr, inv_ipr), j0 = (it - i * ipr) * SW;
+      float pt[PR][PC];
+      const float* src = xs + i * PH * Ws + j0 * PW;
+#pragma unroll
+      for (int u = 0; u < PR; ++u)
+#pragma unroll
+        for (int v = 0; v < PC; ++v) pt[u][v] = src[u * Ws + v];
+#pragma unroll
+      for (int sw = 0; sw < SW; ++sw) {
+        float g = 0.f;
+        if (BWD) {
+          const float g0 = a.gy[ob + (size_t)i * Wq + j0 + sw];
+          g = NP == 1 ? g0 : g0 / (float)NP;
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int u = 0; u < PH; ++u)
+#pragma unroll
+          for (int v = 0; v < PW; ++v) {
+            const int c0 = sw * PW + v;
+            float acc = 0.f;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) acc = fmaf(wr[t], pt[u + t / 3][c0 + t % 3], acc);
+            if (!BWD) {
+              s += fmaxf(acc, 0.f);
+            } else if (!(acc <= 0.f)) {  // ReLU's backward (as stem_kernel)
+#pragma unroll
+              for (int t = 0; t < 9; ++t) dw[t] = fmaf(g, pt[u + t / 3][c0 + t % 3], dw[t]);
+            }
+          }
+        if (!BWD) a.y[ob + (size_t)i * Wq + j0 + sw] = NP == 1 ? s : s / (float)NP;
+      }
+    }
+  }
+  if (!BWD) return;
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 9; ++t) red[threadIdx.x * 9 + t] = dw[t];
+  __syncthreads();
+  if (act && q == 0) {
+    float* pb = a.part + (size_t)blockIdx.x * a.C * 9 + o * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float s = 0.f;
+      for (int k = 0; k < Q; ++k) s += red[(threadIdx.x + k) * 9 + t];
+      pb[t] = s;
+    }
+  }
+}
+
+// launch the stem pass: a compile-time window for res26/res8 pools and no pool
+template <bool BWD>
+static void stem_launch(const StemArgs& a, int grid, hipStream_t st) {
+  const int Wq = a.W / a.pw;
+  if (a.ph == 2 && a.pw == 2) hipLaunchKernelGGL((stem_tile_kernel<BWD, 2, 2, 1>), dim3(grid), dim3(256), 0, st, a);
+  else if (a.ph == 4 && a.pw == 3) hipLaunchKernelGGL((stem_tile_kernel<BWD, 4, 3, 1>), dim3(grid), dim3(256), 0, st, a);
+  else if (a.ph == 1 && a.pw == 1 && Wq % 4 == 0)
+    hipLaunchKernelGGL((stem_tile_kernel<BWD, 1, 1, 4>), dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(stem_kernel<BWD>, dim3(grid), dim3(256), 0, st, a);
+}
+
 static int bn_slices(int B, int C) {
   int S = (4 * 256 + C - 1) / C;  // ~4 workgroups per CU in total
   if (S > B) S = B;
@@ -1105,8 +1515,16 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
   const int np = (int)cdiv((int64_t)a.g.TH * w_, 256);  // output pixels per thread
+  // 19 maps: the LDS-DMA double-buffered MFMA kernel where it applies (d <= 4, W % 4 == 0),
+  // else the register-staged one; HONK_TRAIN_CONV=m / v forces conv3x3m / the VALU kernel
+  // (tests compare all three bitwise)
   const char* ke = getenv("HONK_TRAIN_CONV");
-  if (c == 19 && !(ke && ke[0] == 'v') && train::tm_rows(c, h, w_, dil) > 0) {
+  const int tdr = c == 19 && !(ke && (ke[0] == 'v' || ke[0] == 'm')) ? train::td_rows(c, h, w_, dil) : 0;
+  if (tdr > 0) {
+    a.g = train::class_bands(h, dil, tdr);
+    const int gd = (int)std::min<int64_t>((int64_t)a.B * a.g.nband, cu_count());
+    hipLaunchKernelGGL((train::conv3x3d_kernel<19>), dim3(gd), dim3(512), 0, st, a);
+  } else if (c == 19 && !(ke && ke[0] == 'v') && train::tm_rows(c, h, w_, dil) > 0) {
     a.g = train::class_bands(h, dil, train::tm_rows(c, h, w_, dil));
     const int gm = train::tc_grid((int64_t)a.B * a.g.nband);
     hipLaunchKernelGGL((train::conv3x3m_kernel<19>), dim3(gm), dim3(256), 0, st, a);
@@ -1128,17 +1546,19 @@ namespace {
 // the weight-gradient kernel for a shape: the MFMA one for 19 maps (HONK_TRAIN_CONV=v
 // selects the VALU kernel, for tests), its class-band geometry and grid
 struct WgradPlan {
-  bool mfma;
+  bool mfma, dma;
   train::ClassBands g;
   int grid;
 };
 WgradPlan wgrad_plan(int64_t batch, int c, int h, int w_, int dil) {
   WgradPlan p;
   const char* ke = getenv("HONK_TRAIN_CONV");
+  const int td = c == 19 && !(ke && (ke[0] == 'v' || ke[0] == 'm')) ? train::twd_rows(c, h, w_, dil) : 0;
   const int tw = c == 19 && !(ke && ke[0] == 'v') ? train::tw_rows(c, h, w_, dil) : 0;
-  p.mfma = tw > 0;
-  p.g = train::class_bands(h, dil, p.mfma ? tw : train::tc_rows(c, h, w_, dil));
-  p.grid = train::tc_grid(batch * p.g.nband);
+  p.dma = td > 0;
+  p.mfma = !p.dma && tw > 0;
+  p.g = train::class_bands(h, dil, p.dma ? td : p.mfma ? tw : train::tc_rows(c, h, w_, dil));
+  p.grid = p.dma ? (int)std::min<int64_t>(batch * p.g.nband, cu_count()) : train::tc_grid(batch * p.g.nband);
   return p;
 }
 }  // namespace
@@ -1151,6 +1571,8 @@ extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, i
   int64_t t = batch * train::class_bands(h, dil, train::tc_rows(c, h, w_, dil)).nband;
   const int tw = c == 19 ? train::tw_rows(c, h, w_, dil) : 0;
   if (tw > 0) t = std::max<int64_t>(t, batch * train::class_bands(h, dil, tw).nband);
+  const int td = c == 19 ? train::twd_rows(c, h, w_, dil) : 0;  // grid <= CUs < tc_grid's 2 CUs
+  if (td > 0) t = std::max<int64_t>(t, batch * train::class_bands(h, dil, td).nband);
   return (size_t)train::tc_grid(t) * c * c * 9 * sizeof(float);
 }
 
@@ -1174,12 +1596,13 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
   a.g = wp.g;
   const int grid = wp.grid;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (wp.mfma) hipLaunchKernelGGL((train::wgrad3x3m_kernel<19>), dim3(grid), dim3(256), 0, st, a);
+  if (wp.dma) hipLaunchKernelGGL((train::wgrad3x3d_kernel<19>), dim3(grid), dim3(512), 0, st, a);
+  else if (wp.mfma) hipLaunchKernelGGL((train::wgrad3x3m_kernel<19>), dim3(grid), dim3(256), 0, st, a);
   else if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((train::wgrad3x3_kernel<45>), dim3(grid), dim3(512), 0, st, a);
   tl.done(st);
   HONK_LAUNCH_CHECK("wgrad3x3_kernel");
-  hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, 64)), dim3(256), 0, st, (const float*)workspace, dw,
+  hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, train::WSUM_OUT)), dim3(256), 0, st, (const float*)workspace, dw,
                      n, grid);
   HONK_LAUNCH_CHECK("wsum_kernel");
   return HONK_OK;
@@ -1304,7 +1727,7 @@ extern "C" int honk_res_stem_fwd_f32(const float* x, const float* w0, float* y, 
   if (rc) return rc;
   if (batch == 0) return HONK_OK;
   train::StemArgs a{x, w0, nullptr, y, nullptr, (int)batch, c, h, w_, ph, pw};
-  hipLaunchKernelGGL(train::stem_kernel<false>, dim3(stem_grid(batch)), dim3(256), 0, (hipStream_t)stream, a);
+  train::stem_launch<false>(a, stem_grid(batch), (hipStream_t)stream);
   HONK_LAUNCH_CHECK("stem_kernel");
   return HONK_OK;
 }
@@ -1329,10 +1752,10 @@ extern "C" int honk_res_stem_wgrad_f32(const float* x, const float* w0, const fl
   if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
   const int grid = stem_grid(batch);
   train::StemArgs a{x, w0, gy, nullptr, (float*)workspace, (int)batch, c, h, w_, ph, pw};
-  hipLaunchKernelGGL(train::stem_kernel<true>, dim3(grid), dim3(256), 0, st, a);
+  train::stem_launch<true>(a, grid, st);
   HONK_LAUNCH_CHECK("stem_kernel");
   const int n = c * 9;
-  hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, 64)), dim3(256), 0, st, (const float*)workspace, dw,
+  hipLaunchKernelGGL(train::wsum_kernel, dim3((unsigned)cdiv(n, train::WSUM_OUT)), dim3(256), 0, st, (const float*)workspace, dw,
                      n, grid);
   HONK_LAUNCH_CHECK("wsum_kernel");
   return HONK_OK;

@@ -18,8 +18,9 @@ Forward dispatch:
 * CPU tensors, or training mode (autograd) -> the same PyTorch module ops the
   reference runs (the reference is pure PyTorch; this keeps ``--no_cuda``
   evaluation and ``train()`` working); on ROCm tensors in training mode the
-  block convs (every dilation) and their train-mode BatchNorms run on the native
-  training kernels (``honk_amd/conv3x3.py``).
+  stem (conv0 + relu + avg-pool), the block convs (every dilation) and each
+  block's relu / residual / train-mode BatchNorm run on the native training
+  kernels (``honk_amd/conv3x3.py``); the mean, Linear and loss stay PyTorch.
 """
 from __future__ import annotations
 

@@ -75,44 +75,61 @@ def test_wgrad_deterministic():
     assert torch.equal(hc._wgrad(x, dy), hc._wgrad(x, dy))
 
 
-# bar: relative to the float64 step.  res8 at this seed has a channel that is dead
+# res8 at this seed has a channel that is dead
 # (all <= 0 before ReLU) after conv1 in float64; fp32 rounding differences of
 # ~1e-6 at its exact zeros flip ReLU masks, and train-mode BatchNorm (variance
 # ~0, sigma = sqrt(eps)) amplifies them ~300x per layer in the backward pass
 # (exp/diag_train2.py / diag_train3.py: the native forward is within 1e-6 of
 # float64 at every layer; dgrad and wgrad alone leave every gradient at 1e-6)
-@pytest.mark.parametrize("name,B,bar", [("res26-narrow", 8, 1e-3), ("res8-narrow", 4, 1e-3), ("res8", 6, 1e-2)])
+@pytest.mark.parametrize("name,B,bar", [("res26-narrow", 8, 1e-3), ("res8-narrow", 4, 1e-3), ("res8", 6, 1e-2),
+                                        ("res8-narrow", 16, 2e-5)])
 def test_train_step_grads_match_pytorch(name, B, bar):
-    # float64 CPU step = the reference; every gradient of the native-conv step must
-    # be within 1e-3 relative of it or no farther than the all-PyTorch (MIOpen) fp32
-    # step's (train-mode BatchNorm backward through 24 layers amplifies fp32
-    # rounding: measured native 1-3e-4, MIOpen 1e-3 .. 2e-2 on res26-narrow)
-    torch.manual_seed(0)
-    cfg = dict(hm.find_config(name))
-    m = hm.find_model(name)(cfg).to(DEV).train()
-    g = torch.Generator(device=DEV).manual_seed(1)
-    x = torch.randn(B, 101, 40, device=DEV, generator=g)
-    y = torch.randint(0, cfg["n_labels"], (B,), device=DEV, generator=g)
-
+    # float64 CPU step = the reference; yardsticks = the two other fp32 steps (all-PyTorch
+    # on MIOpen, and the CPU fp32 step -- the reference's own arithmetic).  Train-mode
+    # BatchNorm at small batches makes the step ill-conditioned: a ReLU mask flipped by
+    # one fp32 rounding in a nearly dead channel is amplified up to 1/sqrt(eps) per layer,
+    # so every fp32 implementation lands either ~1e-6 or ~1e-2 from float64 depending on
+    # the draw (exp/diag_stem_noise.py on the GPU, res26-narrow B=8, 4 seeds, max relative
+    # gradient error: native 1.7e-6 / 2.0e-2 / 1.5e-6 / 2.5e-3, MIOpen 7.4e-3 / 2.3e-2 /
+    # 3.9e-3 / 3.8e-2, CPU fp32 2.8e-6 / 2.1e-2 / 2.5e-6 / 1.3e-2).  A single draw is a
+    # coin flip, so over 4 seeds: the native step's median error (max over parameters)
+    # must be within `bar` or 2x the yardsticks' median, and no native draw beyond 2x the
+    # worst yardstick draw.  res8-narrow at B = 16 is well conditioned (every step ~1e-6,
+    # so 2x the yardsticks is far below it): there the 2e-5 bar is the bound.
     def step(mod, xx, yy):
         mod.zero_grad()
         loss = F.cross_entropy(mod(xx), yy)
         loss.backward()
         return loss.detach().double().cpu(), {k: p.grad.detach().double().cpu() for k, p in mod.named_parameters()}
 
-    res = {}
-    for native in (True, False):
-        m.honk_native_train = native
-        res[native] = step(m, x, y)
-    m64 = hm.find_model(name)(cfg).double().train()
-    m64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in m.state_dict().items()})
-    l64, g64 = step(m64, x.double().cpu(), y.cpu())
-    (ln, gn), (lt, gt) = res[True], res[False]
-    assert abs(float(ln - l64)) <= max(3 * abs(float(lt - l64)), 1e-5)
-    for k in g64:
-        en, et = _rel(gn[k], g64[k]), _rel(gt[k], g64[k])
-        print(f"{name} {k}: native {en:.2e}  pytorch-fp32 {et:.2e}")
-        assert en <= max(et, bar), (k, en, et)
+    nat, yard = [], []
+    for seed in range(4):
+        torch.manual_seed(seed)
+        cfg = dict(hm.find_config(name))
+        m = hm.find_model(name)(cfg).to(DEV).train()
+        g = torch.Generator(device=DEV).manual_seed(1 + seed)
+        x = torch.randn(B, 101, 40, device=DEV, generator=g)
+        y = torch.randint(0, cfg["n_labels"], (B,), device=DEV, generator=g)
+        sd = {k: v.clone() for k, v in m.state_dict().items()}
+        res = {}
+        for native in (True, False):
+            m.load_state_dict(sd)
+            m.honk_native_train = native
+            res[native] = step(m, x, y)
+        mc = hm.find_model(name)(cfg).train()
+        mc.load_state_dict({k: v.cpu() for k, v in sd.items()})
+        res["cpu"] = step(mc, x.cpu(), y.cpu())
+        m64 = hm.find_model(name)(cfg).double().train()
+        m64.load_state_dict({k: v.double().cpu() if v.is_floating_point() else v.cpu() for k, v in sd.items()})
+        l64, g64 = step(m64, x.double().cpu(), y.cpu())
+        err = {k: max(_rel(r[1][p], g64[p]) for p in g64) for k, r in res.items()}
+        print(f"{name} B={B} seed {seed}: native {err[True]:.2e}  pytorch-fp32 {err[False]:.2e}  "
+              f"cpu-fp32 {err['cpu']:.2e}")
+        nat.append(err[True])
+        yard.append(max(err[False], err["cpu"]))
+    med = lambda v: sorted(v)[len(v) // 2]
+    assert med(nat) <= max(2 * med(yard), bar), (nat, yard)
+    assert max(nat) <= max(2 * max(yard), bar), (nat, yard)
 
 
 def test_native_train_minimum_batch_and_eval_switch():
@@ -132,22 +149,27 @@ def test_native_train_minimum_batch_and_eval_switch():
     torch.testing.assert_close(gpu, cpu, rtol=0, atol=1e-4)
 
 
-@pytest.mark.parametrize("B,H,W,d", [(3, 50, 20, 1), (2, 101, 40, 2), (3, 101, 40, 4), (2, 101, 40, 16), (2, 9, 5, 3)])
+@pytest.mark.parametrize("B,H,W,d", [(3, 50, 20, 1), (2, 101, 40, 2), (3, 101, 40, 4), (2, 101, 40, 16), (2, 9, 5, 3),
+                                     (300, 50, 20, 1), (2, 7, 4, 1)])
 def test_conv3x3_mfma_bitwise_vs_valu(monkeypatch, B, H, W, d):
-    """The 19-map training conv on fp32 MFMA (conv3x3m_kernel, the default) sums in the
-    VALU kernel's order (k = 9 c + t, an fmaf chain): forward and input gradient are
-    bit-identical to HONK_TRAIN_CONV=v (train-mode BatchNorm makes the step sensitive
+    """The 19-map training convs on fp32 MFMA (conv3x3d_kernel, the default where it
+    applies, and conv3x3m_kernel) sum in the VALU kernel's order (k = 9 c + t, an fmaf
+    chain): forward and input gradient are bit-identical to HONK_TRAIN_CONV=v (train-mode BatchNorm makes the step sensitive
     to any change of rounding, so the order is part of the contract)."""
     g = torch.Generator(device=DEV).manual_seed(7 + H + d)
     x = torch.randn(B, 19, H, W, device=DEV, generator=g)
     w = torch.randn(19, 19, 3, 3, device=DEV, generator=g) * 0.1
     dy = torch.randn(B, 19, H, W, device=DEV, generator=g)
     outs = {}
-    for k in ("m", "v"):
-        monkeypatch.setenv("HONK_TRAIN_CONV", k)
+    for k in ("d", "m", "v"):  # d: the default (LDS-DMA conv3x3d_kernel where d <= 4 and W % 4 == 0)
+        if k == "d":
+            monkeypatch.delenv("HONK_TRAIN_CONV", raising=False)
+        else:
+            monkeypatch.setenv("HONK_TRAIN_CONV", k)
         outs[k] = (hc._conv(x, w, flip=False, d=d), hc._conv(x, w, flip=True, d=d), hc._wgrad(x, dy, d=d))
-    assert torch.equal(outs["m"][0], outs["v"][0])
-    assert torch.equal(outs["m"][1], outs["v"][1])
+    for k in ("d", "m"):
+        assert torch.equal(outs[k][0], outs["v"][0]), k
+        assert torch.equal(outs[k][1], outs["v"][1]), k
     # the weight gradient (wgrad3x3m_kernel) sums the pixels in another order: fp32
     # rounding apart, the same sums (both are within 1e-5 of float64 above)
     assert _rel(outs["m"][2], outs["v"][2]) < 1e-5
