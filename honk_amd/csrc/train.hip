@@ -786,6 +786,11 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3m_kernel(WgradArgs a) {
 // the 16 A lanes of a read hit 16 banks); 8 waves take interleaved k-steps; their
 // partials are summed in wave order, one partial per workgroup (wsum_kernel).
 // ---------------------------------------------------------------------------- //
+// 9 DMA instructions per wave per tile: two 72-KB buffers (144 of the CU's 160 KB), a
+// 17-row band for res26-narrow (8 k-steps of 4 px per wave were 8 -> 10.6 per tile)
+constexpr int TWD_ITER = 9;
+constexpr int TWD_BUF = 8 * TWD_ITER * 1024;
+
 __host__ __device__ inline int twd_ds(int TH, int W) {  // dy plane stride (floats)
   const int f = TH * W;
   return f + ((4 - f % 64) + 64) % 64;
@@ -799,7 +804,7 @@ template <int C>
 __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   static_assert(C <= 20, "wgrad3x3d_kernel: C <= 20");
   constexpr int K9 = 9 * C, NJ = (K9 + 15) / 16, NO = (C + 15) / 16;
-  __shared__ __attribute__((aligned(16))) float tdl[2 * TD_BUF / 4];
+  __shared__ __attribute__((aligned(16))) float tdl[2 * TWD_BUF / 4];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i16 = lane & 15, kk = lane >> 4;
@@ -821,10 +826,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   // per lane and DMA instruction i: chunk e -> x chunk (plane c, row rr: image row
   // hr + rr d) or dy chunk (plane o, band row jr: image row r + (k0 + jr) d), as the
   // byte offset in its clip tensor at row 0 and the band row; kind 0 = zero chunk
-  int cbase[TD_ITER], crow[TD_ITER], ckind[TD_ITER];
+  int cbase[TWD_ITER], crow[TWD_ITER], ckind[TWD_ITER];
 #pragma unroll
-  for (int i = 0; i < TD_ITER; ++i) {
-    const int e = (wave * TD_ITER + i) * 64 + lane, f = e * 4;
+  for (int i = 0; i < TWD_ITER; ++i) {
+    const int e = (wave * TWD_ITER + i) * 64 + lane, f = e * 4;
     cbase[i] = 0;
     crow[i] = 0;
     ckind[i] = 0;
@@ -856,7 +861,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.dy + (size_t)b * clip), (short)0, (int)(clip * 4), 0x00020000);
     const int hb = r + k0 * d;
 #pragma unroll
-    for (int i = 0; i < TD_ITER; ++i) {
+    for (int i = 0; i < TWD_ITER; ++i) {
       const int h = hb + crow[i] * d;
       const bool ok = ckind[i] != 0 && h >= 0 && h < H && (ckind[i] == 1 || crow[i] < th);
       const unsigned voff = ok ? (unsigned)(cbase[i] + h * W * 4) : 0x80000000u;
@@ -865,16 +870,16 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
       // exec masks, every slot written once
       if (ckind[i] == 2)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rd, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TD_ITER + i) * 256)),
+            rd, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TWD_ITER + i) * 256)),
             16, voff, 0, 0, 0);
       else
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rx, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TD_ITER + i) * 256)),
+            rx, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TWD_ITER + i) * 256)),
             16, voff, 0, 0, 0);
     }
   };
   float* buf0 = tdl;
-  float* buf1 = tdl + TD_BUF / 4;
+  float* buf1 = tdl + TWD_BUF / 4;
   if ((int)blockIdx.x < ntile) issue(blockIdx.x, buf0);
   const float invW = 1.0f / (float)W;
   int it = 0;
@@ -936,7 +941,7 @@ static int twd_rows(int C, int H, int W, int d) {
   const int hc = (H + d - 1) / d;
   int th = 0;
   for (int t = 1; t <= hc; ++t) {
-    if (twd_nchunk(C, W, t) > 8 * TD_ITER * 64 || C * td_geo(C, W, t).PS >= 65536) break;
+    if (twd_nchunk(C, W, t) > 8 * TWD_ITER * 64 || C * td_geo(C, W, t).PS >= 65536) break;
     th = t;
   }
   if (th < 1) return 0;
