@@ -114,16 +114,51 @@ def _route(stream, is_rank0):
     stream.close()
 
 
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def count_gpus_sysfs(root=None, env=None):
+    """Visible GPUs counted WITHOUT the HIP runtime: KFD topology nodes whose
+    properties carry a non-zero gfx_target_version (CPU nodes carry 0), capped by
+    the visibility lists ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES.  None when the topology is unreadable (the ranks then
+    check LOCAL_RANK against their own device count)."""
+    root = root or os.environ.get("HONK_KFD_TOPOLOGY", KFD_TOPOLOGY)
+    env = os.environ if env is None else env
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(root, node, "properties")) as f:
+                props = dict(ln.split(None, 1) for ln in f if len(ln.split(None, 1)) == 2)
+        except OSError:
+            continue
+        try:
+            if int(props.get("gfx_target_version", "0").strip()) != 0:
+                n += 1
+        except ValueError:
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
+
+
 def spawn_ranks(n, argv, script=None):
     """Start n rank processes of this script and wait for them; returns the exit status.
 
     A rank that fails ends the others (they would otherwise wait in a collective).
-    Called before anything touches the GPU (torch.cuda.device_count() does not
-    initialise HIP on this image)."""
+    This process never initialises HIP (no torch.cuda call at all): the GPUs are
+    counted from the KFD topology in sysfs, and each rank also checks its
+    LOCAL_RANK against its own device count (rank_main)."""
     import threading
     if not os.environ.get("HONK_BENCH_ONE_GPU"):
-        have = torch.cuda.device_count()
-        if have < n:
+        have = count_gpus_sysfs()
+        if have is not None and have < n:
             log(f"--gpus {n} but only {have} visible GPU(s)")
             return 2
     script = script or os.path.abspath(__file__)
@@ -487,6 +522,9 @@ def rank_main(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    if not os.environ.get("HONK_BENCH_ONE_GPU") and local >= torch.cuda.device_count():
+        log(f"LOCAL_RANK {local} but only {torch.cuda.device_count()} visible GPU(s)")
+        sys.exit(2)
     if dist:
         import torch.distributed as tdist
         # rehearsal knobs for a 1-GPU box (never set by the driver): HONK_BENCH_BACKEND=gloo

@@ -57,6 +57,7 @@ _PROTOS = {
                                          ctypes.c_float, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p]),
     "honk_conv3x3_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 5
                          + [ctypes.c_void_p]),
+    "honk_conv3x3_check": (ctypes.c_int, [ctypes.c_int32] * 4),
     "honk_conv3x3_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64] + [ctypes.c_int32] * 4),
     "honk_conv3x3_wgrad_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 4
                                + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
@@ -165,5 +166,5 @@ def res_launch_plan(desc, batch: int, n_cus: int = 0):
     kinds = (ctypes.c_int32 * 256)()
     n = lib.honk_res_launch_plan(ctypes.byref(desc), int(batch), int(n_cus), kinds, 256)
     if n < 0:
-        check(-n, "honk_res_launch_plan")
+        check(n, "honk_res_launch_plan")
     return [KERNEL_NAMES[kinds[i]] for i in range(min(n, 256))]

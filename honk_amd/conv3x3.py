@@ -23,11 +23,30 @@ CHANNELS = (19, 45)
 
 def supported(x, conv) -> bool:
     """The native kernels cover bias-free 3x3 convs with padding == dilation (the res
-    blocks' "same" convs) and C in CHANNELS."""
+    blocks' "same" convs) whose (C, H, W, dilation) the library accepts
+    (honk_conv3x3_check, host-only: C in CHANNELS, the band plan fits)."""
     d = tuple(conv.dilation)
-    return (x.is_cuda and x.dtype == torch.float32 and conv.weight.shape[0] in CHANNELS
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.weight.shape[0] in CHANNELS
             and tuple(conv.kernel_size) == (3, 3) and d[0] == d[1] and 1 <= d[0] <= 64
-            and tuple(conv.padding) == d and tuple(conv.stride) == (1, 1) and conv.bias is None)
+            and tuple(conv.padding) == d and tuple(conv.stride) == (1, 1) and conv.bias is None):
+        return False
+    return _native.load().honk_conv3x3_check(int(conv.weight.shape[0]), int(x.shape[2]), int(x.shape[3]),
+                                             int(d[0])) == 0
+
+
+_warned = set()
+
+
+def warn_fallback(model, what):
+    """Say once per (model, reason) that a training step left the native kernels, so
+    a configuration outside their envelope is not silently slow."""
+    key = (id(model), what)
+    if key in _warned:
+        return
+    _warned.add(key)
+    import warnings
+    warnings.warn(f"honk_amd: {type(model).__name__} training falls back to PyTorch/MIOpen for {what}",
+                  RuntimeWarning, stacklevel=3)
 
 
 def _conv(x, w, flip, d=1):

@@ -1132,8 +1132,8 @@ size_t honk_res_packed_floats(const honk_res_desc* d) {
 int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, int32_t* kinds, int32_t max_kinds) {
   Layout L;
   int rc = make_layout(d, &L);
-  if (rc) return -rc;
-  if (batch < 1) return -fail(HONK_ERR_ARG, "batch < 1");
+  if (rc) return rc;
+  if (batch < 1) return fail(HONK_ERR_ARG, "batch < 1");
   const int64_t n = chunk_clips(L, batch);
   int grid = n_cus > 0 ? n_cus : cu_count();
   if (grid > n) grid = (int)n;
@@ -1147,7 +1147,7 @@ int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, i
     return cnt;
   }
   const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;
-  if (plan_block16r(L, SP).TH == 0) return -fail(HONK_ERR_UNSUPPORTED, "width beyond the row-band staging plan");
+  if (plan_block16r(L, SP).TH == 0) return fail(HONK_ERR_UNSUPPORTED, "width beyond the row-band staging plan");
   if (!use_w_kernel(L, d, SP)) {
     for (int i = 1; i <= L.L; ++i) put(HONK_KERNEL_ROWBAND);
     return cnt;

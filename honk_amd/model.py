@@ -168,6 +168,11 @@ class SpeechResModel(SerializableModule):
                 # conv0, relu and the avg-pool as one native stem
                 x = old_x = _conv3x3.stem(x_in, conv, pool)
                 continue
+            if native_convs and i == 0:
+                _conv3x3.warn_fallback(self, "the stem (conv0 + relu + pool)")
+            if native_convs and i > 0 and not _conv3x3.supported(x, conv):
+                _conv3x3.warn_fallback(self, f"the block convs ({conv.weight.shape[0]} maps, "
+                                             f"{tuple(x.shape[2:])} map, dilation {conv.dilation[0]})")
             if native_convs and i > 0 and _conv3x3.supported(x, conv) and \
                     _conv3x3.bn_supported(x, getattr(self, "bn{}".format(i))):
                 # conv, then relu / residual add / train BatchNorm as one fused tail
@@ -198,6 +203,8 @@ class SpeechResModel(SerializableModule):
                 if native_convs and _conv3x3.bn_supported(x, bn):
                     x = _conv3x3.batch_norm_train(x, bn)
                 else:
+                    if native_convs and bn.training:
+                        _conv3x3.warn_fallback(self, "train-mode BatchNorm")
                     x = bn(x)
         x = x.view(x.size(0), x.size(1), -1)  # shape: (batch, feats, o3)
         x = torch.mean(x, 2)

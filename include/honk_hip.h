@@ -71,8 +71,8 @@ size_t honk_res_packed_floats(const honk_res_desc* d);
 size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch);
 /*
  * The block-layer launches honk_res_forward makes per batch chunk, in order: kinds[i]
- * = HONK_KERNEL_* (up to max_kinds written).  Returns the launch count, or minus a
- * status code.  n_cus = 0: the current device's CU count (the pair kernel's plan
+ * = HONK_KERNEL_* (up to max_kinds written).  Returns the launch count (> 0), or a
+ * (negative) HONK_ERR_* status code.  n_cus = 0: the current device's CU count (the pair kernel's plan
  * depends on clips per workgroup).  Host-only; no GPU work.
  */
 #define HONK_KERNEL_BLOCK_F32 1 /* fp32-MFMA layer (block_kernel)                        */
@@ -163,6 +163,9 @@ int honk_sgd_step_f32(float* params, const float* grads, float* momentum_buf, in
  */
 int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h, int32_t w_,
                      int32_t dil, int32_t flip, void* stream);
+/* Host-only: HONK_OK when honk_conv3x3_f32 / honk_conv3x3_wgrad_f32 cover (C, H, W, dil),
+ * else the status (and honk_last_error text) those calls would return. */
+int honk_conv3x3_check(int32_t c, int32_t h, int32_t w_, int32_t dil);
 /* dw[o][i][ky][kx] = sum_{b,h,w} dy[b][o][h][w] * x[b][i][h+(ky-1)d][w+(kx-1)d] (zero padded);
  * deterministic: per-workgroup partials in the workspace, summed in a fixed order. */
 size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil);

@@ -86,3 +86,55 @@ def test_train_flops_res26_narrow():
     cfg = dict(hm.find_config("res26-narrow"))
     # 157.33 MFLOP forward, training ~3x forward - conv0 dgrad ~ 471 MFLOP
     assert abs(bench.train_flops_per_clip(cfg) / 1e6 - 471) < 2
+
+
+def _fake_topology(root, gfx_versions):
+    for i, v in enumerate(gfx_versions):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count {0 if v else 16}\nsimd_count {1024 if v else 0}\n"
+                                      f"gfx_target_version {v}\n")
+
+
+def test_count_gpus_sysfs(tmp_path):
+    _fake_topology(tmp_path, [0, 90500, 90500, 90500])
+    assert bench.count_gpus_sysfs(str(tmp_path), env={}) == 3
+    assert bench.count_gpus_sysfs(str(tmp_path), env={"HIP_VISIBLE_DEVICES": "0,1"}) == 2
+    assert bench.count_gpus_sysfs(str(tmp_path), env={"ROCR_VISIBLE_DEVICES": "2"}) == 1
+    assert bench.count_gpus_sysfs(str(tmp_path / "missing"), env={}) is None
+
+
+def test_spawn_parent_never_initialises_hip(tmp_path):
+    """The --gpus N parent counts GPUs from sysfs only: with every torch.cuda entry
+    that could reach the HIP runtime (amdsmi path included) made to fail, the parent
+    still launches the ranks and torch.cuda stays uninitialised in it; too few GPUs
+    in the topology end the job with status 2 before any rank starts."""
+    topo = tmp_path / "topo"
+    _fake_topology(topo, [0, 90500, 90500])
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys\nprint('{\"rank\": %s}' % os.environ['RANK'])\n")
+    drv = textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {REPO!r})
+        import torch
+        def _boom(*a, **k):
+            raise AssertionError("HIP touched by the launcher")
+        torch.cuda.device_count = _boom
+        torch.cuda.is_available = _boom
+        torch.cuda._lazy_init = _boom
+        torch._C._cuda_getDeviceCount = _boom
+        import bench
+        rc = bench.spawn_ranks(int(sys.argv[1]), ['--gpus', sys.argv[1]], script={str(script)!r})
+        assert not torch.cuda.is_initialized()
+        sys.exit(rc)
+    """)
+    env = dict(os.environ, HONK_KFD_TOPOLOGY=str(topo))
+    for k in ("HONK_BENCH_ONE_GPU", "WORLD_SIZE", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+              "CUDA_VISIBLE_DEVICES"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-c", drv, "2"], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.strip() == '{"rank": 0}'
+    p = subprocess.run([sys.executable, "-c", drv, "3"], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2, p.stderr
+    assert "only 2 visible GPU(s)" in p.stderr

@@ -257,3 +257,34 @@ def test_res_launch_plan_host_only(monkeypatch):
     assert plan("res15", "bf16x3") == ["block16w_kernel"] * 13
     monkeypatch.setenv("HONK_RES_KERNEL", "r")
     assert plan("res15", "bf16x3") == ["block16r_kernel"] * 13
+
+
+def test_res_launch_plan_errors_raise_with_reason():
+    """A descriptor the kernels cannot run returns a negative HONK_ERR_* status from
+    honk_res_launch_plan (not a launch count): the binding raises RuntimeError with
+    the library's reason."""
+    from honk_amd import _native
+    from honk_amd import model as hm
+    m = hm.find_model("res15")(dict(hm.find_config("res15")))
+    m.honk_precision = "bf16x3"
+    with pytest.raises(RuntimeError, match="width|staging plan"):
+        _native.res_launch_plan(m._desc(101, 67), 4, n_cus=256)
+    with pytest.raises(RuntimeError, match="batch"):
+        _native.res_launch_plan(m._desc(101, 40), 0, n_cus=256)
+    bad = m._desc(101, 40)
+    bad.n_maps = 0
+    with pytest.raises(RuntimeError, match="status -"):
+        _native.res_launch_plan(bad, 4, n_cus=256)
+
+
+def test_conv3x3_check_host_only():
+    """honk_conv3x3_check: the training convs' envelope as a host-only query, which
+    conv3x3.supported() asks before dispatching (45 maps at dilation 64 on W=40 does
+    not fit the band plan: PyTorch conv then, not a RuntimeError mid-step)."""
+    from honk_amd import _native
+    lib = _native.load()
+    assert lib.honk_conv3x3_check(19, 50, 20, 1) == 0
+    assert lib.honk_conv3x3_check(45, 101, 40, 16) == 0
+    assert lib.honk_conv3x3_check(45, 101, 40, 64) == -2
+    assert lib.honk_conv3x3_check(32, 101, 40, 1) == -2
+    assert lib.honk_conv3x3_check(19, 101, 40, 0) == -1

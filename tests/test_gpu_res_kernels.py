@@ -116,6 +116,8 @@ def test_pair_kernel_bitwise_vs_w(monkeypatch, name, override, B, prec):
     params, x = _case(cfg, B, seed=31)
     m = _module(cfg, params, name, prec)
     monkeypatch.setenv("HONK_RES_KERNEL", "p")
+    # the case must really run the pair kernel (else 'p' would compare 'w' with itself)
+    assert "block16p_kernel" in _native.res_launch_plan(m._desc(101, 40), B)
     outp = _run(m, x)
     monkeypatch.setenv("HONK_RES_KERNEL", "w")
     outw = _run(m, x)
