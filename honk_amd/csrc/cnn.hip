@@ -55,6 +55,10 @@ typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4c __attribute__((ext_vector_type(4)));
 constexpr int BKP = BK + 8;  // X3 LDS row pitch (bf16): 80 B keeps 16-lane fragment reads conflict-free
 
+// max / relu with torch's NaN behaviour (a NaN propagates)
+__device__ __forceinline__ float nanmax(float m, float v) { return (v > m || v != v) ? v : m; }
+__device__ __forceinline__ float relu_nan(float v) { return v <= 0.f ? 0.f : v; }
+
 template <bool POOL2, bool X3>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
   // fp32: Ws[2][BK][BN + PADM], Xs[2][BK][BM + PADM] (floats)
@@ -248,10 +252,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + i * 16 + (lane >> 4) * 4 + r;
         float v = acc[i][j][r] + ((a.bias && n < a.N) ? a.bias[n] : 0.f);
-        if (a.relu) v = fmaxf(v, 0.f);
-        if (POOL2) {  // max over the 2x2 window = lanes l, l^1, l^2, l^3 (same n)
-          v = fmaxf(v, __shfl_xor(v, 1));
-          v = fmaxf(v, __shfl_xor(v, 2));
+        if (a.relu) v = v <= 0.f ? 0.f : v;  // NaN passes, as torch.relu
+        if (POOL2) {  // max over the 2x2 window = lanes l, l^1, l^2, l^3 (same n); NaN propagates
+          v = nanmax(v, __shfl_xor(v, 1));
+          v = nanmax(v, __shfl_xor(v, 2));
           if (a.nhwc_x3) pooled[r] = v;
           else if ((lane & 3) == 0 && mok && n < a.N) a.out[obase + (int64_t)n * plane] = v;
         } else if (mok && n < a.N) {
@@ -432,7 +436,7 @@ __global__ __launch_bounds__(256, 1) void conv2x3_kernel(Conv2X3Args a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int n = (2 * ng + j) * 16 + 4 * g + r;
-            if (n < a.N) ob[(size_t)n * ohw + p] = fmaxf(acc[m][j][r] + a.bias[n], 0.f);
+            if (n < a.N) ob[(size_t)n * ohw + p] = relu_nan(acc[m][j][r] + a.bias[n]);
           }
       }
     }
@@ -560,9 +564,9 @@ __global__ __launch_bounds__(512, 1) void conv1x3_kernel(Conv1X3Args a) {
       bf16x4c hv, lv;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = fmaxf(acc[j][r], 0.f);
-        v = fmaxf(v, __shfl_xor(v, 1));
-        v = fmaxf(v, __shfl_xor(v, 2));
+        float v = relu_nan(acc[j][r]);
+        v = nanmax(v, __shfl_xor(v, 1));
+        v = nanmax(v, __shfl_xor(v, 2));
         hv[r] = (__bf16)v;
         lv[r] = (__bf16)(v - (float)hv[r]);
       }
@@ -758,7 +762,7 @@ __global__ __launch_bounds__(256) void linear_small_kernel(const float* __restri
     const int c = tid / NB, n = tid - c * NB;
     if (n < N && r0 + c < m) {
       float v = red[0][c][n] + red[1][c][n] + red[2][c][n] + red[3][c][n] + (b ? b[n] : 0.f);
-      if (relu) v = fmaxf(v, 0.f);
+      if (relu) v = relu_nan(v);
       y[(r0 + c) * N + n] = v;
     }
   }
@@ -789,6 +793,243 @@ static int maxpool(const float* in, float* out, int64_t planes, int h, int w, in
                      kh, kw);
   HONK_LAUNCH_CHECK("maxpool_kernel");
   return HONK_OK;
+}
+
+
+// ---------------------------------------------------------------------------- //
+// SpeechModel training (utils/train.py:123-135 on the cnn configs: the backward of
+// model.py:186-193).  The forward reuses conv_gemm_kernel (conv + bias + ReLU,
+// pre-pool output kept for the backward) and maxpool_kernel; dropout stays
+// PyTorch's own op between them (the reference's RNG stream and mask semantics).
+//   * max-pool backward: the gradient of each window goes to its first maximum in
+//     scan order (the forward's rule, v > m || isnan(v): torch's max_pool2d index);
+//   * weight + bias gradient: dW[n][k] = sum_m g'[n][m] X[k][m], k = (ci, kh, kw),
+//     m = (clip, oh, ow), g' = the output gradient through the ReLU (act > 0), X
+//     gathered from the NCHW input (the forward's im2col), on fp32 MFMA with m as
+//     the reduction; the m range is split over workgroups (one partial each) and
+//     the partials are summed in a fixed order: deterministic;
+//   * input gradient (stride 1): the full correlation of g' with the flipped,
+//     transposed weights = conv_gemm_kernel over g' zero-padded by (KH-1, KW-1).
+// ---------------------------------------------------------------------------- //
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ in, const float* __restrict__ gout,
+                                                          float* __restrict__ gin, int64_t planes, int H, int W,
+                                                          int KH, int KW) {
+  const int PH = H / KH, PW = W / KW;
+  const int64_t total = planes * H * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % W);
+    const int64_t t = i / W;
+    const int y = (int)(t % H);
+    const int64_t pl = t / H;
+    const int ph = y / KH, pw = x / KW;
+    float g = 0.f;
+    if (ph < PH && pw < PW) {
+      const float* p = in + pl * H * W + (int64_t)(ph * KH) * W + pw * KW;
+      float m = p[0];
+      int best = 0;
+      for (int u = 0; u < KH; ++u)
+        for (int v = 0; v < KW; ++v) {
+          const float e = p[u * W + v];
+          if (e > m || e != e) {
+            m = e;
+            best = u * KW + v;
+          }
+        }
+      if (best == (y - ph * KH) * KW + (x - pw * KW)) g = gout[(pl * PH + ph) * PW + pw];
+    }
+    gin[i] = g;
+  }
+}
+
+constexpr int WG_BN = 64;  // out channels per workgroup
+constexpr int WG_BK = 64;  // (ci, kh, kw) columns per workgroup
+constexpr int WG_BM = 32;  // reduction (m) per LDS stage
+
+struct ConvWgradArgs {
+  const float* in;   // [B][Cin][H][W]
+  const float* gy;   // [B][N][OH][OW]
+  const float* act;  // [B][N][OH][OW] ReLU output (g' = act <= 0 ? 0 : gy), or nullptr
+  float* part;       // [S][N][K]
+  float* pbias;      // [S][N] or nullptr
+  int64_t M, mper;   // B*OH*OW; m per split (multiple of WG_BM)
+  int N, K, Cin, H, W, KH, KW, SH, SW, OH, OW;
+};
+
+// 256 threads = 4 waves; wave w owns out channels n0 + 16w .. +15 and all 4
+// 16-column tiles of the workgroup's 64 k (4 accumulators).  A stage stages 32 m
+// of g' ([m][n]) and X ([m][k]) in LDS, the next stage's global loads in flight
+// during the 8 k-steps of v_mfma_f32_16x16x4_f32.  Staging: thread = m column
+// (tid & 31) x 8 rows (tid >> 5) + 8j, one (clip, pixel) decomposition per stage.
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
+  __shared__ float Gs[2][WG_BM][WG_BN + 4];
+  __shared__ float Xs[2][WG_BM][WG_BK + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * WG_BN, k0 = blockIdx.y * WG_BK, sp = blockIdx.z;
+  const int64_t mbeg = (int64_t)sp * a.mper;
+  const int64_t mend = mbeg + a.mper < a.M ? mbeg + a.mper : a.M;
+  const int mc = tid & 31, r8 = tid >> 5;
+  const int KHW = a.KH * a.KW, OHW = a.OH * a.OW;
+  int koff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + r8 + 8 * j;
+    if (k < a.K) {
+      const int ci = k / KHW, rem = k - ci * KHW;
+      const int kh = rem / a.KW, kw = rem - kh * a.KW;
+      koff[j] = (ci * a.H + kh) * a.W + kw;
+    } else {
+      koff[j] = -1;
+    }
+  }
+  const bool do_bias = a.pbias != nullptr && blockIdx.y == 0;
+  float gv[8], xv[8], bsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+  auto load = [&](int64_t m0) {
+    const int64_t m = m0 + mc;
+    const bool ok = m < mend;
+    int64_t gbase = 0, xbase = 0;
+    if (ok) {
+      const int64_t b = m / OHW;
+      const int pix = (int)(m - b * OHW);
+      const int oh = pix / a.OW, ow = pix - oh * a.OW;
+      gbase = b * (int64_t)a.N * OHW + pix;
+      xbase = b * (int64_t)a.Cin * a.H * a.W + (int64_t)(oh * a.SH) * a.W + ow * a.SW;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + r8 + 8 * j;
+      float g = 0.f;
+      if (ok && n < a.N) {
+        const int64_t o = gbase + (int64_t)n * OHW;
+        g = a.gy[o];
+        if (a.act && a.act[o] <= 0.f) g = 0.f;  // threshold_backward: NaN passes
+      }
+      gv[j] = g;
+      xv[j] = (ok && koff[j] >= 0) ? a.in[xbase + koff[j]] : 0.f;
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bsum[j] += gv[j];
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      Gs[buf][mc][r8 + 8 * j] = gv[j];
+      Xs[buf][mc][r8 + 8 * j] = xv[j];
+    }
+  };
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nst = mend > mbeg ? (mend - mbeg + WG_BM - 1) / WG_BM : 0;
+  if (nst > 0) {
+    load(mbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < nst; ++t) {
+    const int buf = (int)(t & 1);
+    if (t + 1 < nst) load(mbeg + (t + 1) * WG_BM);
+#pragma unroll
+    for (int ks = 0; ks < WG_BM / 4; ++ks) {
+      const int kk = ks * 4 + (lane >> 4);
+      const float av = Gs[buf][kk][wave * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Xs[buf][kk][j * 16 + (lane & 15)], acc[j], 0, 0, 0);
+    }
+    if (t + 1 < nst) store(buf ^ 1);
+    __syncthreads();
+  }
+  // D[i][jj]: lane holds rows i = (lane >> 4) * 4 + r (out channel), column jj = lane & 15 (k)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = k0 + j * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + wave * 16 + (lane >> 4) * 4 + r;
+      if (n < a.N && k < a.K) a.part[((int64_t)sp * a.N + n) * a.K + k] = acc[j][r];
+    }
+  }
+  if (do_bias) {
+    // the 32 lanes of a half-wave share r8: tree over the m columns
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = bsum[j];
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+      const int n = n0 + r8 + 8 * j;
+      if (mc == 0 && n < a.N) a.pbias[(int64_t)sp * a.N + n] = v;
+    }
+  }
+}
+
+// out[i] = sum over s of part[s][i], s ascending (fixed order: deterministic)
+__global__ __launch_bounds__(256) void split_sum_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                        int64_t n, int S) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[(int64_t)s * n + i];
+  out[i] = v;
+}
+
+// gp[pl][y][x] = g'[pl][y - (KH-1)][x - (KW-1)] inside the map, else 0 (g' = ReLU-masked gy)
+__global__ __launch_bounds__(256) void dgrad_pad_kernel(const float* __restrict__ gy, const float* __restrict__ act,
+                                                        float* __restrict__ gp, int64_t planes, int OH, int OW,
+                                                        int PHp, int PWp, int KH, int KW) {
+  const int64_t total = planes * PHp * PWp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % PWp);
+    const int64_t t = i / PWp;
+    const int y = (int)(t % PHp);
+    const int64_t pl = t / PHp;
+    const int oy = y - (KH - 1), ox = x - (KW - 1);
+    float g = 0.f;
+    if (oy >= 0 && oy < OH && ox >= 0 && ox < OW) {
+      const int64_t o = (pl * OH + oy) * OW + ox;
+      g = gy[o];
+      if (act && act[o] <= 0.f) g = 0.f;
+    }
+    gp[i] = g;
+  }
+}
+
+// wf[ci][n][kh][kw] = w[n][ci][KH-1-kh][KW-1-kw]
+__global__ __launch_bounds__(256) void flip_weights_kernel(const float* __restrict__ w, float* __restrict__ wf, int N,
+                                                           int Cin, int KH, int KW) {
+  const int KHW = KH * KW;
+  const int64_t total = (int64_t)N * Cin * KHW;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int t = (int)(i % KHW);
+  const int64_t q = i / KHW;
+  const int n = (int)(q % N);
+  const int ci = (int)(q / N);
+  wf[i] = w[((int64_t)n * Cin + ci) * KHW + (KHW - 1 - t)];
+}
+
+struct WgradPlanC {
+  int tn, tk, S;
+  int64_t M, mper;
+};
+static WgradPlanC wgrad_plan_c(int64_t batch, int cin, int h, int w, int cout, int kh, int kw, int sh, int sw) {
+  WgradPlanC p;
+  const int oh = (h - kh) / sh + 1, ow = (w - kw) / sw + 1;
+  p.M = batch * oh * ow;
+  p.tn = (int)cdiv(cout, WG_BN);
+  p.tk = (int)cdiv((int64_t)cin * kh * kw, WG_BK);
+  int64_t S = cdiv(1024, (int64_t)p.tn * p.tk);          // ~4 workgroups per CU
+  const int64_t smax = cdiv(p.M, 8 * WG_BM);             // >= 8 stages per split
+  if (S > smax) S = smax;
+  if (S > 4096) S = 4096;
+  if (S < 1) S = 1;
+  p.mper = cdiv(cdiv(p.M, S), WG_BM) * WG_BM;
+  p.S = (int)cdiv(p.M, p.mper);
+  if (p.S < 1) p.S = 1;
+  return p;
 }
 
 struct Shapes {
@@ -876,6 +1117,105 @@ int honk_linear_f32(const float* x, const float* w, const float* b, float* y, in
   if (m == 0) return HONK_OK;
   if (!x || !w || !y) return fail(HONK_ERR_ARG, "null pointer argument");
   return linear(x, w, b, y, m, k, n, relu, (hipStream_t)stream);
+}
+
+int honk_maxpool2d_bwd_f32(const float* in, const float* gout, float* gin, int64_t batch, int32_t c, int32_t h,
+                           int32_t w, int32_t kh, int32_t kw, void* stream) {
+  if (!in || !gout || !gin) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 0 || c < 1 || kh < 1 || kw < 1 || kh > h || kw > w)
+    return fail(HONK_ERR_ARG, "bad pool %dx%d on %dx%d", kh, kw, h, w);
+  const int64_t total = batch * c * h * w;
+  if (total == 0) return HONK_OK;
+  const int64_t blocks = cdiv(total, 256) < 65536 ? cdiv(total, 256) : 65536;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in, gout, gin,
+                     batch * c, h, w, kh, kw);
+  HONK_LAUNCH_CHECK("maxpool_bwd_kernel");
+  return HONK_OK;
+}
+
+static int conv_train_check(int64_t batch, int cin, int h, int w, int cout, int kh, int kw, int sh, int sw) {
+  if (batch < 0 || cin < 1 || cout < 1 || kh < 1 || kw < 1 || sh < 1 || sw < 1 || kh > h || kw > w)
+    return fail(HONK_ERR_ARG, "bad conv geometry (cin=%d %dx%d k=%dx%d s=%dx%d cout=%d)", cin, h, w, kh, kw, sh, sw,
+                cout);
+  return HONK_OK;
+}
+
+size_t honk_conv2d_wgrad_workspace_bytes(int64_t batch, int32_t cin, int32_t h, int32_t w, int32_t cout, int32_t kh,
+                                         int32_t kw, int32_t sh, int32_t sw) {
+  if (batch < 1 || conv_train_check(batch, cin, h, w, cout, kh, kw, sh, sw) != HONK_OK) return 0;
+  const WgradPlanC p = wgrad_plan_c(batch, cin, h, w, cout, kh, kw, sh, sw);
+  return (size_t)p.S * ((size_t)cout * cin * kh * kw + cout) * sizeof(float);
+}
+
+int honk_conv2d_wgrad_f32(const float* in, const float* gy, const float* act, float* dw, float* db, int64_t batch,
+                          int32_t cin, int32_t h, int32_t w, int32_t cout, int32_t kh, int32_t kw, int32_t sh,
+                          int32_t sw, void* workspace, size_t ws_bytes, void* stream) {
+  int rc = conv_train_check(batch, cin, h, w, cout, kh, kw, sh, sw);
+  if (rc) return rc;
+  if (!in || !gy || !dw) return fail(HONK_ERR_ARG, "null pointer argument");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t K = (int64_t)cin * kh * kw;
+  if (batch == 0) {
+    HONK_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)cout * K * sizeof(float), st));
+    if (db) HONK_HIP_CHECK(hipMemsetAsync(db, 0, (size_t)cout * sizeof(float), st));
+    return HONK_OK;
+  }
+  const size_t need = honk_conv2d_wgrad_workspace_bytes(batch, cin, h, w, cout, kh, kw, sh, sw);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  const WgradPlanC p = wgrad_plan_c(batch, cin, h, w, cout, kh, kw, sh, sw);
+  ConvWgradArgs a;
+  a.in = in; a.gy = gy; a.act = act;
+  a.part = (float*)workspace;
+  a.pbias = db ? a.part + (int64_t)p.S * cout * K : nullptr;
+  a.M = p.M; a.mper = p.mper;
+  a.N = cout; a.K = (int)K; a.Cin = cin; a.H = h; a.W = w; a.KH = kh; a.KW = kw; a.SH = sh; a.SW = sw;
+  a.OH = (h - kh) / sh + 1; a.OW = (w - kw) / sw + 1;
+  {
+    TimedLaunch tl(st, 2.0 * (double)p.M * cout * K);
+    hipLaunchKernelGGL(conv_wgrad_kernel, dim3(p.tn, p.tk, p.S), dim3(256), 0, st, a);
+    tl.done(st);
+  }
+  HONK_LAUNCH_CHECK("conv_wgrad_kernel");
+  const int64_t nw = (int64_t)cout * K;
+  hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)cdiv(nw, 256)), dim3(256), 0, st, a.part, dw, nw, p.S);
+  if (db)
+    hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)cdiv(cout, 256)), dim3(256), 0, st, a.pbias, db,
+                       (int64_t)cout, p.S);
+  HONK_LAUNCH_CHECK("split_sum_kernel");
+  return HONK_OK;
+}
+
+size_t honk_conv2d_dgrad_workspace_bytes(int64_t batch, int32_t cin, int32_t h, int32_t w, int32_t cout, int32_t kh,
+                                         int32_t kw) {
+  if (batch < 1 || conv_train_check(batch, cin, h, w, cout, kh, kw, 1, 1) != HONK_OK) return 0;
+  const int64_t oh = h - kh + 1, ow = w - kw + 1;
+  const int64_t php = oh + 2 * (kh - 1), pwp = ow + 2 * (kw - 1);
+  return (size_t)(batch * cout * php * pwp + (int64_t)cout * cin * kh * kw) * sizeof(float);
+}
+
+int honk_conv2d_dgrad_f32(const float* gy, const float* act, const float* w, float* dx, int64_t batch, int32_t cin,
+                          int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw, void* workspace,
+                          size_t ws_bytes, void* stream) {
+  int rc = conv_train_check(batch, cin, h, w_, cout, kh, kw, 1, 1);
+  if (rc) return rc;
+  if (!gy || !w || !dx) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch == 0) return HONK_OK;
+  const size_t need = honk_conv2d_dgrad_workspace_bytes(batch, cin, h, w_, cout, kh, kw);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  const int oh = h - kh + 1, ow = w_ - kw + 1;
+  const int php = oh + 2 * (kh - 1), pwp = ow + 2 * (kw - 1);
+  float* gp = (float*)workspace;
+  float* wf = gp + batch * cout * (int64_t)php * pwp;
+  const int64_t np = batch * cout * (int64_t)php * pwp;
+  const int64_t blocks = cdiv(np, 256) < 65536 ? cdiv(np, 256) : 65536;
+  hipLaunchKernelGGL(dgrad_pad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, gy, act, gp, batch * cout, oh, ow,
+                     php, pwp, kh, kw);
+  HONK_LAUNCH_CHECK("dgrad_pad_kernel");
+  const int64_t nw = (int64_t)cout * cin * kh * kw;
+  hipLaunchKernelGGL(flip_weights_kernel, dim3((unsigned)cdiv(nw, 256)), dim3(256), 0, st, w, wf, cout, cin, kh, kw);
+  HONK_LAUNCH_CHECK("flip_weights_kernel");
+  return conv(gp, wf, nullptr, dx, batch, cout, php, pwp, cin, kh, kw, 1, 1, 0, st);
 }
 
 size_t honk_cnn_workspace_bytes(const honk_cnn_desc* d, int64_t batch) {

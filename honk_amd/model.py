@@ -20,7 +20,9 @@ Forward dispatch:
   evaluation and ``train()`` working); on ROCm tensors in training mode the
   stem (conv0 + relu + avg-pool), the block convs (every dilation) and each
   block's relu / residual / train-mode BatchNorm run on the native training
-  kernels (``honk_amd/conv3x3.py``); the mean, Linear and loss stay PyTorch.
+  kernels (``honk_amd/conv3x3.py``), and so do SpeechModel's relu(conv) layers
+  and max-pools (``honk_amd/cnn_train.py``); dropout, the mean, the Linear
+  layers and the loss stay PyTorch.
 """
 from __future__ import annotations
 
@@ -31,6 +33,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import cnn_train as _cnn_train
 from . import conv3x3 as _conv3x3
 
 
@@ -359,16 +362,35 @@ class SpeechModel(SerializableModule):
         # "f32": fp32 MFMA; "bf16x3": operands split into bf16 hi/lo pairs on the
         # bf16 MFMA pipe (same 1e-4 logit bar; tests/test_gpu_cnn_x3.py)
         self.honk_precision = "f32"
+        # training on ROCm tensors: convs + ReLU and max-pools on the gfx950 kernels (False: MIOpen)
+        self.honk_native_train = True
 
     # -- reference forward (CPU tensors / training mode): model.py:186-205 --
-    def _torch_forward(self, x):
-        x = F.relu(self.conv1(x.unsqueeze(1)))  # shape: (batch, channels, i1, o1)
+    # native: training on a ROCm tensor runs relu(conv) and the max-pools on the
+    # native training kernels (honk_amd/cnn_train.py); dropout, the Linear layers and
+    # the loss stay PyTorch autograd on the device
+    def _conv_relu(self, conv, x, native):
+        if native and _cnn_train.conv_supported(x, conv):
+            return _cnn_train.conv_relu(x, conv)
+        if native:
+            _conv3x3.warn_fallback(self, f"{tuple(conv.weight.shape)} conv")
+        return F.relu(conv(x))
+
+    def _pool(self, pool, x, native):
+        if native and _cnn_train.pool_supported(x, pool):
+            return _cnn_train.max_pool(x, pool)
+        if native:
+            _conv3x3.warn_fallback(self, f"MaxPool2d({pool.kernel_size})")
+        return pool(x)
+
+    def _torch_forward(self, x, native=False):
+        x = self._conv_relu(self.conv1, x.unsqueeze(1), native)  # shape: (batch, channels, i1, o1)
         x = self.dropout(x)
-        x = self.pool1(x)
+        x = self._pool(self.pool1, x, native)
         if hasattr(self, "conv2"):
-            x = F.relu(self.conv2(x))  # shape: (batch, o1, i2, o2)
+            x = self._conv_relu(self.conv2, x, native)  # shape: (batch, o1, i2, o2)
             x = self.dropout(x)
-            x = self.pool2(x)
+            x = self._pool(self.pool2, x, native)
         x = x.view(x.size(0), -1)  # shape: (batch, o3)
         if hasattr(self, "lin"):
             x = self.lin(x)
@@ -426,7 +448,7 @@ class SpeechModel(SerializableModule):
     def forward(self, x):
         if _native_ready(x, self):
             return self._native_forward(x)
-        return self._torch_forward(x)
+        return self._torch_forward(x, native=x.is_cuda and self.honk_native_train)
 
 
 def _pair(v):

@@ -130,6 +130,34 @@ int honk_maxpool2d_f32(const float* in, float* out, int64_t batch, int32_t c, in
 int honk_linear_f32(const float* x, const float* w, const float* b, float* y, int64_t m, int32_t k,
                     int32_t n, int32_t relu, void* stream);
 
+/* ---- SpeechModel training (utils/train.py:123-135 on the cnn configs) ----------- */
+/*
+ * The backward of model.py:186-193 (relu(conv) -> dropout -> max-pool; the forward is
+ * honk_conv2d_f32 with relu = 1 and honk_maxpool2d_f32), replacing the cuDNN/MIOpen
+ * convolution backward and max_pool2d_with_indices_backward autograd runs there.
+ * g' below is the output gradient gy through the ReLU: g' = (act <= 0 ? 0 : gy), act =
+ * the forward's ReLU output (act may be NULL: g' = gy) -- torch's threshold_backward.
+ *
+ * Max-pool backward (MaxPool2d((kh,kw)), stride = kernel, floor): gin = gout at each
+ * window's first maximum in scan order (v > m || isnan(v): torch's index), 0 elsewhere.
+ */
+int honk_maxpool2d_bwd_f32(const float* in, const float* gout, float* gin, int64_t batch, int32_t c, int32_t h,
+                           int32_t w, int32_t kh, int32_t kw, void* stream);
+/* dw[n][ci][kh][kw] = sum_{b,oh,ow} g'[b][n][oh][ow] * in[b][ci][oh*sh+kh][ow*sw+kw]; db[n] = sum g' (db may
+ * be NULL).  fp32 MFMA; deterministic (per-split partials in the workspace, summed in fixed order). */
+size_t honk_conv2d_wgrad_workspace_bytes(int64_t batch, int32_t cin, int32_t h, int32_t w, int32_t cout, int32_t kh,
+                                         int32_t kw, int32_t sh, int32_t sw);
+int honk_conv2d_wgrad_f32(const float* in, const float* gy, const float* act, float* dw, float* db, int64_t batch,
+                          int32_t cin, int32_t h, int32_t w, int32_t cout, int32_t kh, int32_t kw, int32_t sh,
+                          int32_t sw, void* workspace, size_t workspace_bytes, void* stream);
+/* stride 1: dx[b][ci][y][x] = sum_{n,kh,kw} g'[b][n][y-kh][x-kw] * w[n][ci][kh][kw] (zero outside g'),
+ * dx [batch][cin][h][w]; the full correlation as an fp32-MFMA implicit GEMM over g' padded in the workspace */
+size_t honk_conv2d_dgrad_workspace_bytes(int64_t batch, int32_t cin, int32_t h, int32_t w, int32_t cout, int32_t kh,
+                                         int32_t kw);
+int honk_conv2d_dgrad_f32(const float* gy, const float* act, const float* w, float* dx, int64_t batch, int32_t cin,
+                          int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
 /* ---- MFCC front-end (AudioPreprocessor.compute_mfccs, utils/manage_audio.py:30-42) ---- */
 /*
  * pcm [batch][samples] f32 -> out [batch][1 + samples/hop][n_dct] f32 (the

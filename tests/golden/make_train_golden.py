@@ -48,6 +48,24 @@ DP_CASES = [
     # name, model, batch (split in 2 shards), lr, momentum, weight_decay, nesterov, seed
     ("train_dp2_res26-narrow", "res26-narrow", 8, 0.1, 0.9, 1e-5, False, 304),
 ]
+# Compact cases at the reference's own batch (utils/train.py:171 batch_size=64):
+# inputs and labels are NOT stored -- they regenerate from the PCG64 seed (checked
+# against the stored float64 sum / sum of squares) -- and parameters are stored
+# after the last step only (every step's loss and gradients are stored).
+# Overrides are merged into the reference config before the model is built; the cnn
+# cases set dropout_prob = 0 so the step is RNG-free (dropout semantics are tested
+# separately, on the device, against PyTorch's own dropout).
+COMPACT_CASES = [
+    # name, model, overrides, batch, steps, lr, momentum, weight_decay, nesterov, seed
+    ("train_res26-narrow-b64", "res26-narrow", {}, 64, 2, 0.1, 0.9, 1e-5, False, 305),
+    ("train_cnn-trad-pool2-b64", "cnn-trad-pool2", dict(dropout_prob=0.0), 64, 2, 0.01, 0.9, 1e-5, False, 306),
+    ("train_cnn-one-fstride4-b64", "cnn-one-fstride4", dict(dropout_prob=0.0, n_labels=12), 64, 2, 0.01, 0.9,
+     1e-5, True, 307),
+]
+COMPACT_DP_CASES = [
+    # name, model, batch (split in 2 shards of 32), lr, momentum, weight_decay, nesterov, seed
+    ("train_dp2_res26-narrow-b64", "res26-narrow", 64, 0.1, 0.9, 1e-5, False, 308),
+]
 
 
 def _model(mod, name, params):
@@ -55,6 +73,10 @@ def _model(mod, name, params):
     m = mod.find_model(name)(cfg)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     return cfg, m
+
+
+def _x_check(x):
+    return np.array([float(np.sum(x, dtype=np.float64)), float(np.sum(np.square(x, dtype=np.float64)))])
 
 
 def _inputs(seed, batch, n_labels):
@@ -148,6 +170,86 @@ def main():
             out[f"b0__{k}"] = v
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
         print(f"{name:26s} B={batch} shard losses={losses}")
+    compact(mod, crit)
+
+
+def compact(mod, crit):
+    import json
+    for name, model_name, over, batch, steps, lr, mom, wd, nest, seed in COMPACT_CASES:
+        cfg0 = dict(mod.find_config(model_name))
+        cfg0.update(over)
+        x, y, rng = _inputs(seed, batch, cfg0["n_labels"])
+        if "n_layers" in cfg0:
+            params = _params(cfg0, seed, rng)
+        else:
+            params = orc.make_params(cfg0, seed)
+        model = mod.find_model(model_name)(dict(cfg0))
+        model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+        opt = torch.optim.SGD(model.parameters(), lr=lr, nesterov=nest, weight_decay=wd, momentum=mom)
+        out = dict(model=np.array(model_name), overrides=np.array(json.dumps(over, sort_keys=True)),
+                   seed=np.array(seed), batch=np.array(batch), x_check=_x_check(x),
+                   y_check=np.array(int(np.sum(y * (np.arange(batch) + 1)))), lr=np.array(lr),
+                   momentum=np.array(mom), weight_decay=np.array(wd), nesterov=np.array(nest), steps=np.array(steps),
+                   keys=np.array([k for k, _ in model.named_parameters()]), checksum=orc.params_checksum(params))
+        for k, v in params.items():
+            if "running_" in k:
+                out[f"init__{k}"] = np.asarray(v, np.float32)
+        losses = []
+        for s in range(steps):
+            model.train()
+            opt.zero_grad()
+            loss = crit(model(torch.from_numpy(x)), torch.from_numpy(y))
+            loss.backward()
+            for k, p in model.named_parameters():
+                out[f"g{s}__{k}"] = p.grad.detach().numpy().copy()
+            opt.step()
+            losses.append(float(loss.item()))
+            if s == steps - 1:
+                for k, p in model.named_parameters():
+                    out[f"p{s}__{k}"] = p.detach().numpy().copy()
+            for k, v in _buffers(model).items():
+                out[f"b{s}__{k}"] = v
+        out["loss"] = np.array(losses, np.float64)
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+        print(f"{name:30s} B={batch} steps={steps} losses={losses}")
+
+    for name, model_name, batch, lr, mom, wd, nest, seed in COMPACT_DP_CASES:
+        cfg0 = dict(mod.find_config(model_name))
+        x, y, rng = _inputs(seed, batch, cfg0["n_labels"])
+        params = _params(cfg0, seed, rng)
+        half = batch // 2
+        grads, losses, bufs0 = [], [], None
+        for r in range(2):
+            cfg, m = _model(mod, model_name, params)
+            m.train()
+            sl = slice(r * half, (r + 1) * half)
+            loss = crit(m(torch.from_numpy(x[sl])), torch.from_numpy(y[sl]))
+            loss.backward()
+            grads.append({k: p.grad.detach().numpy().copy() for k, p in m.named_parameters()})
+            losses.append(float(loss.item()))
+            if r == 0:
+                bufs0 = _buffers(m)
+        cfg, m = _model(mod, model_name, params)
+        opt = torch.optim.SGD(m.parameters(), lr=lr, nesterov=nest, weight_decay=wd, momentum=mom)
+        opt.zero_grad()
+        for k, p in m.named_parameters():
+            p.grad = torch.from_numpy((grads[0][k] + grads[1][k]) / 2)
+        opt.step()
+        out = dict(model=np.array(model_name), overrides=np.array("{}"), seed=np.array(seed), batch=np.array(batch),
+                   x_check=_x_check(x), y_check=np.array(int(np.sum(y * (np.arange(batch) + 1)))), lr=np.array(lr),
+                   momentum=np.array(mom), weight_decay=np.array(wd), nesterov=np.array(nest),
+                   keys=np.array([k for k, _ in m.named_parameters()]), checksum=orc.params_checksum(params),
+                   shard_loss=np.array(losses, np.float64))
+        for k, v in params.items():
+            if "running_" in k:
+                out[f"init__{k}"] = np.asarray(v, np.float32)
+        for k, p in m.named_parameters():
+            out[f"gmean__{k}"] = ((grads[0][k] + grads[1][k]) / 2).astype(np.float32)
+            out[f"p0__{k}"] = p.detach().numpy().copy()
+        for k, v in bufs0.items():
+            out[f"b0__{k}"] = v
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+        print(f"{name:30s} B={batch} shard losses={losses}")
 
 
 if __name__ == "__main__":

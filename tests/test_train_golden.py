@@ -1,20 +1,31 @@
 """Training parity pinned to the REFERENCE: tests/golden/train_*.npz hold the
-reference's own train step (SpeechResModel in train mode, CrossEntropyLoss,
-torch.optim.SGD with momentum / weight decay / nesterov as in
-/root/reference/utils/train.py:99,125-135), made by make_train_golden.py.
+reference's own train step (SpeechResModel / SpeechModel in train mode,
+CrossEntropyLoss, torch.optim.SGD with momentum / weight decay / nesterov as in
+/root/reference/utils/train.py:99,125-135), made by make_train_golden.py; the
+compact fixtures run the reference's default batch of 64 (train.py:171) on
+res26-narrow (config C5), cnn-trad-pool2 and cnn-one-fstride4 (dropout_prob 0).
 
-* CPU: honk_amd's module + FlatSGD reproduce it bit for bit (same torch CPU ops).
+* CPU: honk_amd's module + FlatSGD reproduce every fixture bit for bit (same torch
+  CPU ops).
 * CPU, 2 ranks over gloo: the data-parallel step (broadcast, ONE all-reduce of the
   flat bucket, SGD on the mean) reproduces the reference's 2-shard mean-gradient
   step (train_dp2_*.npz, DDP semantics of config C5).
-* GPU: the native training path (gfx950 block-conv fwd / dgrad / wgrad at every
-  dilation, train-BN kernels, fused SGD) is at least as accurate as the
-  reference's own fp32 step: per step, its gradients (max |err| / max |grad| per
-  tensor), updated weights, loss and running stats are no farther from the
-  float64 step than 2x the reference fp32's distance (floors 1e-4 / 1e-6 / 1e-5 /
-  1e-5).  A plain fp32 tolerance does not work here: on res26-narrow the
-  reference's own fp32 gradients are 1.5e-2 from float64 (train-mode BatchNorm of
-  a 4-clip batch divides by near-zero batch variances of almost-dead channels).
+* The bound.  A training step is piecewise smooth: every ReLU mask and max-pool
+  index is a discrete decision, and fp32 rounding in another summation order flips
+  a few of the ~1e7 decisions of a 64-clip step, each moving a weight gradient by
+  ~1/sqrt(B*H*W) (tests/decision_replay.py).  The reference's own fp32 step is
+  1.1e-2 (res26-narrow-b64) / 2.2e-3 (cnn-trad-pool2-b64) from float64 for that
+  reason, so no fp32 implementation can be held to 1e-4 on raw gradients.  The
+  tight statement is per decision set: the step under test equals the float64
+  step taken with ITS OWN decisions to gradients <= 1e-4 relative (max |err| /
+  max |grad| per tensor), parameters <= 1e-6 absolute, loss <= 1e-5, running
+  stats <= 1e-5 relative -- and the harness is pinned by the reference: its fp32
+  steps sit within 1.1e-5 of their decision-matched float64 steps (below).
+* GPU: the native training path (res: stem, block convs fwd / dgrad / wgrad,
+  fused relu + residual + train BN; cnn: conv + ReLU, max-pool, their backward;
+  fused SGD) meets that bound on every step of every fixture, with no fallback,
+  the loss of the first step within 1e-5 of the fixture, and fewer than 1e-5 of
+  its decisions different from the reference's.
 """
 import os
 import socket
@@ -25,13 +36,17 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+import decision_replay as dr
 import train_golden_util as tg
 from honk_amd import distributed as hd
 from honk_amd.optim import FlatParams, FlatSGD
 
 
 
-@pytest.mark.parametrize("name", tg.TRAIN_CASES)
+ALL_CASES = tg.TRAIN_CASES + tg.COMPACT_CASES
+
+
+@pytest.mark.parametrize("name", ALL_CASES)
 def test_cpu_train_step_bitwise_vs_reference(name):
     z, out = tg.replay(name, "cpu")
     assert tg.compare(z, out, 0, 0, 0, 0) == [0.0, 0.0, 0.0, 0.0]
@@ -91,14 +106,91 @@ def test_dp2_step_vs_reference_shard_mean():
         np.testing.assert_array_equal(res[0][2][k], res[1][2][k])   # replicas stay identical
 
 
+def _opt_args(z):
+    return dict(lr=float(z["lr"]), momentum=float(z["momentum"]), weight_decay=float(z["weight_decay"]),
+                nesterov=bool(z["nesterov"]))
+
+
+def _record_step(m, x, y):
+    dec = dr.Decisions()
+    m.train()
+    with dr.record(dec):
+        loss = torch.nn.CrossEntropyLoss()(m(x), y)
+    return dec, loss
+
+
+@pytest.mark.parametrize("name", ALL_CASES)
+def test_decision_matched_replay_pins_reference(name):
+    """The harness against the reference: the fixture's fp32 step (= this package's CPU
+    step, bit for bit) recorded, replayed in float64 with its own decisions: the
+    reference's gradients within 1e-4 relative (observed <= 1.1e-5) and its loss
+    within 1e-6 -- against 1e-3..1e-2 for the undecided float64 step."""
+    z = tg.load(name)
+    cfg, m = tg.build(z, "cpu")
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    x, y = tg.inputs(z)
+    dec, _ = _record_step(m, torch.from_numpy(x), torch.from_numpy(y))
+    r = dr.replay_step(cfg, str(z["model"]), state, x, y, dec, _opt_args(z))
+    assert r["ambiguous"] == 0
+    assert abs(r["loss"] - float(z["loss"][0])) <= 1e-6
+    for k in r["g"]:
+        assert dr.rel_err(z[f"g0__{k}"], r["g"][k]) <= 1e-4, k
+
+
+def _bucket_views(flat, buf):
+    out, off = {}, 0
+    for k, p in flat.named:
+        n = p.numel()
+        out[k] = buf[off:off + n].view_as(p)
+        off += n
+    return out
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", tg.TRAIN_CASES)
+@pytest.mark.parametrize("name", ALL_CASES)
 def test_gpu_native_train_step_vs_reference(name):
-    z, out = tg.replay(name, "cuda:0")
-    rows = tg.compare_vs_f64(z, out, tg.replay_f64(name))
-    print(name, "per step (got, bound) for grad rel / param abs / loss abs / running-stat rel:", rows)
-    # the fp32 loss of the first step is the reference's within fp32 reassociation
-    assert abs(out["loss"][0] - float(z["loss"][0])) <= 1e-5
+    """Every step of the fixture on the native GPU path, each against the float64 step
+    with the GPU's own decisions (bounds in the module docstring), from the GPU's
+    state before that step (parameters, running stats, momentum buffer)."""
+    import warnings
+    z = tg.load(name)
+    cfg, m = tg.build(z, "cuda:0")
+    flat = FlatParams(m)
+    flat.named = list(m.named_parameters())
+    opt = FlatSGD(flat, **_opt_args(z))
+    xn, yn = tg.inputs(z)
+    x, y = torch.from_numpy(xn).to("cuda:0"), torch.from_numpy(yn).to("cuda:0")
+    # the reference's decisions (CPU path == reference bit for bit) for the first step
+    _, mc = tg.build(z, "cpu")
+    dec_ref, _ = _record_step(mc, torch.from_numpy(xn), torch.from_numpy(yn))
+    rows = []
+    for s in range(int(z["steps"])):
+        state = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        mom = {k: v.clone() for k, v in _bucket_views(flat, opt.buf).items()} if s > 0 else None
+        opt.zero_grad()
+        with warnings.catch_warnings():
+            warnings.simplefilter("error", RuntimeWarning)   # a fallback warning fails the test
+            dec, loss = _record_step(m, x, y)
+            loss.backward()
+        g = {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}
+        opt.step()
+        p_after = {k: p.detach().cpu().numpy().copy() for k, p in m.named_parameters()}
+        b_after = {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items() if "running_" in k}
+        r = dr.replay_step(cfg, str(z["model"]), state, xn, yn, dec, _opt_args(z), momentum_buf=mom)
+        got = (max(dr.rel_err(g[k], r["g"][k]) for k in g),
+               max(float(np.abs(p_after[k] - r["p"][k]).max()) for k in p_after),
+               abs(float(loss.item()) - r["loss"]),
+               max((dr.rel_err(b_after[k], r["b"][k]) for k in b_after), default=0.0))
+        rows.append(got)
+        assert r["ambiguous"] == 0
+        for v, bound, what in zip(got, (1e-4, 1e-6, 1e-5, 1e-5), ("grad", "param", "loss", "running stats")):
+            assert v <= bound, f"step {s} {what}: {v:.3e} > {bound:.0e} vs the decision-matched float64 step"
+        if s == 0:
+            assert abs(float(loss.item()) - float(z["loss"][0])) <= 1e-5
+            nflip = dr.flips(dec, dec_ref)
+            print(name, "decisions", dec.count(), "differing from the reference's:", nflip)
+            assert nflip <= 1e-5 * dec.count()
+    print(name, "per step (grad rel, param abs, loss abs, running-stat rel):", rows)
 
 
 def test_reference_fp32_vs_float64_conditioning():
@@ -108,3 +200,77 @@ def test_reference_fp32_vs_float64_conditioning():
         z = tg.load(name)
         rows = tg.compare_vs_f64(z, None, tg.replay_f64(name), factor=1.0, floors=(1, 1, 1, 1))
         assert rows
+
+
+def _dp_gpu_worker(rank, world, port, name, out):
+    """One rank of the 2-rank data-parallel step on cuda:0 (gloo): the native training
+    kernels on the rank's shard, ONE all-reduce of the flat bucket, the fused SGD;
+    the rank's local gradient checked here against its shard's decision-matched
+    float64 step."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    z = tg.load(name)
+    cfg, m = tg.build(z, "cuda:0")
+    if rank == 1:   # a different starting point on rank 1: the broadcast must replace it
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(1.0)
+    hd.broadcast_module(m)
+    state = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    flat = FlatParams(m)
+    opt = FlatSGD(flat, **_opt_args(z))
+    xn, yn = tg.inputs(z)
+    s, e = hd.shard_bounds(xn.shape[0], rank, world)
+    opt.zero_grad()
+    hd.broadcast_module(m, buffers_only=True)
+    dec, loss = _record_step(m, torch.from_numpy(xn[s:e]).to("cuda:0"), torch.from_numpy(yn[s:e]).to("cuda:0"))
+    loss.backward()
+    local = {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}
+    scale = hd.allreduce_grads(flat)
+    opt.step(grad_scale=scale)
+    r = dr.replay_step(cfg, str(z["model"]), state, xn[s:e], yn[s:e], dec, _opt_args(z))
+    gerr = max(dr.rel_err(local[k], r["g"][k]) for k in local)
+    out[rank] = (float(loss.item()), gerr, r["ambiguous"], local,
+                 {k: p.detach().cpu().numpy().copy() for k, p in m.named_parameters()},
+                 {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items() if "running_" in k},
+                 {k: v.cpu().numpy() for k, v in state.items()})
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_dp2_native_step_vs_reference():
+    """Config C5's data-parallel step through the NATIVE kernels: 2 ranks on cuda:0
+    over gloo (the one-GPU arrangement of bench.py --gpus 2), the reference's 2 x 32
+    shard fixture (train_dp2_res26-narrow-b64): each shard's loss within 1e-5 of the
+    reference's, each rank's local gradient within 1e-4 of its decision-matched
+    float64 step, the update = SGD on the mean of the two local gradients (float64
+    replay, 1e-6), replicas bitwise equal, rank 0's running stats within 1e-5 of the
+    reference's."""
+    name = "train_dp2_res26-narrow-b64"
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_dp_gpu_worker, args=(2, port, name, out), nprocs=2, join=True)
+        res = dict(out)
+    z = tg.load(name)
+    for r in (0, 1):
+        loss, gerr, amb, _, _, _, _ = res[r]
+        assert abs(loss - float(z["shard_loss"][r])) <= 1e-5, (r, loss)
+        assert gerr <= 1e-4 and amb == 0, (r, gerr, amb)
+    for k in res[0][4]:
+        np.testing.assert_array_equal(res[0][4][k], res[1][4][k])   # replicas stay identical
+    for k in res[0][5]:
+        assert tg.rel_err(res[0][5][k], z[f"b0__{k}"]) <= 1e-5, k
+    # the update: torch.optim.SGD (float64) on the mean of the two ranks' local gradients
+    cfg = tg.config(z)
+    from honk_amd import model as hm
+    m = hm.find_model(str(z["model"]))(dict(cfg)).double()
+    m.load_state_dict({k: torch.from_numpy(v).double() if v.dtype != np.int64 else torch.from_numpy(v)
+                       for k, v in res[0][6].items()})
+    opt = torch.optim.SGD(m.parameters(), **_opt_args(z))
+    for k, p in m.named_parameters():
+        p.grad = torch.from_numpy((res[0][3][k].astype(np.float64) + res[1][3][k]) / 2)
+    opt.step()
+    for k, p in m.named_parameters():
+        assert float(np.abs(res[0][4][k] - p.detach().numpy()).max()) <= 1e-6, k
