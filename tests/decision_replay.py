@@ -20,9 +20,8 @@ recorded mask, max-pool = gather at the recorded index), then the optimizer step
 On the same piece of the piecewise-smooth function the two must agree to fp32
 rounding times the step's smooth conditioning (~7 for res26-narrow).
 
-Sites: SpeechResModel -- the stem ReLU (native stem: not observable, float64 decides
-and the replay counts ambiguous pre-activations, |v| < 1e-6 max|v|, which must be 0)
-and every block's ReLU; SpeechModel -- relu(conv1), relu(conv2), the dnn1 ReLU and
+Sites: SpeechResModel -- the stem ReLU (the native stem's mask observed by an unpooled
+run of the same kernel) and every block's ReLU; SpeechModel -- relu(conv1), relu(conv2), the dnn1 ReLU and
 the max-pools.  Reference lines: model.py:104-121 (res), :186-205 (cnn).
 """
 from __future__ import annotations
@@ -40,7 +39,7 @@ from honk_amd import model as hm
 
 class Decisions:
     def __init__(self):
-        self.relu = []   # bool masks (CPU) or None (native stem: not observable)
+        self.relu = []   # bool masks (CPU), or None: not observed (the replay decides, counting ambiguity)
         self.pool = []   # int64 flat indices per pooled output (CPU) or None for a 1x1 pool
 
     def count(self):
@@ -73,7 +72,10 @@ def record(dec: Decisions):
         return h
 
     def stem(x, conv0, pool=None):
-        dec.relu.append(None)
+        # the native stem fuses conv0 + ReLU + avg-pool; its ReLU mask is observed by
+        # running the same kernel family unpooled (the same 9-tap fmaf chain per pixel,
+        # the same relu_f decision), whose output IS relu(conv0)
+        dec.relu.append((orig_stem(x, conv0, None) > 0).detach().cpu())
         return orig_stem(x, conv0, pool)
 
     def crelu(x, conv):
