@@ -33,7 +33,8 @@ struct GemmArgs {
   int Cin, H, W, KH, KW, SH, SW, OH, OW;
   int PH, PW;        // pooled output dims (pool2 fused)
   int relu;
-  int nhwc_x3;       // POOL2 only: store [B][PH][PW][hi N | lo N] bf16 (conv2x3_kernel's input) instead of NCHW fp32
+  int nhwc_x3;       // POOL2 only: 1 = store [B][PH][PW][hi N | lo N] bf16 (conv2x3_kernel's input),
+                     // 2 = [B][PH][PW][N] fp32 (conv2f_kernel's input), instead of NCHW fp32
 };
 
 // D[n][m] = act(bias[n] + sum_k W[n][k] * X[k][m]) on v_mfma_f32_16x16x4_f32.
@@ -262,7 +263,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
           a.out[obase + (int64_t)n * plane] = v;
         }
       }
-      if (POOL2 && a.nhwc_x3 && (lane & 3) == 0 && mok) {
+      if (POOL2 && a.nhwc_x3 == 2 && (lane & 3) == 0 && mok) {
+        // the lane's 4 consecutive channels of its pooled pixel: one 16-B NHWC store
+        const int n = n0 + i * 16 + (lane >> 4) * 4;
+        if (n + 3 < a.N)
+          *(f32x4*)(a.out + (m >> 2) * (int64_t)a.N + n) = f32x4{pooled[0], pooled[1], pooled[2], pooled[3]};
+      }
+      if (POOL2 && a.nhwc_x3 == 1 && (lane & 3) == 0 && mok) {
         // the lane's 4 consecutive channels of its pooled pixel, split into bf16
         // (hi, lo) runs of the [hi N | lo N] pixel (N == 64: host-checked)
         const int n = n0 + i * 16 + (lane >> 4) * 4;
@@ -466,6 +473,153 @@ __global__ void pack_conv2x3_kernel(const float* __restrict__ w, __bf16* __restr
 
 
 // ---------------------------------------------------------------------------- //
+// The same conv2 in fp32 (HONK_PREC_F32, config C2 as BASELINE.json names it) on
+// v_mfma_f32_16x16x4_f32: the conv2x3_kernel design -- the whole clip one tile, two
+// 32-channel half images by LDS-DMA (fp32 NHWC input from conv_gemm_kernel's
+// nhwc_x3 = 2 epilogue: the half image is 128 B per pixel, the bf16 hi/lo one's
+// size), 16-B chunks XOR-swizzled by pixel, 4 waves = 2 out-tile pairs x 2 groups
+// of MT m-tiles, accumulators for the whole clip in VGPRs.
+//   k-chunk (tap t, q): lane group g reads chunk 4q + g of its pixel (channels
+//   32h + 16q + 4g .. +3 as one 16-B read); MFMA e = 0..3 takes element e, so one
+//   read feeds 4 MFMAs per out tile; the weight A operand of MFMA e is
+//   W[co][32h + 16q + 4g + e][t], pre-packed per lane as one float4 per chunk and
+//   out tile (pack_conv2f_kernel, L2-resident), loaded one chunk ahead with the
+//   activations.  fp32 products and accumulation: the fmaf chain of the reference
+//   conv in another order (1e-4 parity).
+// ---------------------------------------------------------------------------- //
+struct Conv2FArgs {
+  const float* in;      // [B][PH][PW][64] fp32
+  const f32x4* wfrag;   // [2 h][ntap][2 q][4 out tiles][64 lanes]
+  const float* bias;    // [N]
+  float* out;           // [B][N][OH][OW]
+  int B, PH, PW, KW, ntap, OH, OW, N;
+};
+
+template <int MT>
+__global__ __launch_bounds__(256, 1) void conv2f_kernel(Conv2FArgs a) {
+  __shared__ __attribute__((aligned(16))) char img[C2X3_IMG];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ng = wave & 1, mg = wave >> 1;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int npx = a.PH * a.PW;
+  const int ohw = a.OH * a.OW;
+  const int chunks = npx * 8;
+  const int pieces = (chunks + 63) / 64;
+  const int clip_bytes = npx * 256;
+
+  int P0[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int p = (mg * MT + m) * 16 + i16;
+    const int oh = p / a.OW, ow = p - oh * a.OW;
+    P0[m] = p < ohw ? oh * a.PW + ow : 0;
+  }
+  const f32x4* wl = a.wfrag + ng * 2 * 64 + lane;
+
+  typedef f32x4 BFr[MT];
+  typedef f32x4 WFr[2];
+  auto loadB = [&](BFr& Bv, int delta, int q) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int P = P0[m] + delta;
+      Bv[m] = *(const f32x4*)(img + (((P << 3) + ((4 * q + g) ^ (P & 7))) << 4));
+    }
+  };
+  auto loadW = [&](WFr& Wv, int c) {  // c = (h * ntap + t) * 2 + q
+#pragma unroll
+    for (int j = 0; j < 2; ++j) Wv[j] = wl[(c * 4 + j) * 64];
+  };
+  f32x4 acc[MT][2];
+  auto mma = [&](const BFr& Bv, const WFr& Wv) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wv[j][e], Bv[m][e], acc[m][j], 0, 0, 0);
+  };
+  auto delta = [&](int t) {
+    const int kh = t / a.KW;
+    return kh * a.PW + (t - kh * a.KW);
+  };
+
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)a.in + (size_t)b * clip_bytes), (short)0, clip_bytes, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();  // every wave is done reading the previous image
+      for (int pc = wave; pc < pieces; pc += 4) {
+        const int st = __builtin_amdgcn_readfirstlane(min(pc * 64, chunks - 64));
+        const int L = st + lane;
+        const int P = L >> 3, c = (L & 7) ^ (P & 7);
+        const unsigned voff = (unsigned)(P * 256 + h * 128 + c * 16);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + st * 16), 16,
+                                                 voff, 0, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces landed
+      __syncthreads();                     // ... and every wave's
+      const int nch = 2 * a.ntap;          // chunks of this half: (tap, q)
+      const int c0 = h * nch;
+      BFr B0, B1;
+      WFr W0, W1;
+      loadW(W0, c0);
+      loadB(B0, 0, 0);
+      for (int c = 0; c < nch; c += 2) {  // chunk c: tap c / 2, q = 0; c + 1: q = 1
+        const int dt = delta(c >> 1);
+        loadW(W1, c0 + c + 1);
+        loadB(B1, dt, 1);
+        mma(B0, W0);
+        if (c + 2 < nch) {
+          loadW(W0, c0 + c + 2);
+          loadB(B0, delta((c >> 1) + 1), 0);
+        }
+        mma(B1, W1);
+      }
+    }
+    float* ob = a.out + (size_t)b * a.N * ohw;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int p = (mg * MT + m) * 16 + i16;
+      if (p < ohw) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = (2 * ng + j) * 16 + 4 * g + r;
+            if (n < a.N) ob[(size_t)n * ohw + p] = relu_nan(acc[m][j][r] + a.bias[n]);
+          }
+      }
+    }
+  }
+}
+
+// conv2 weights [N][64][KH][KW] fp32 -> conv2f_kernel's fragments: chunk
+// c = (h * ntap + t) * 2 + q, out tile nt, lane (g, i16): the float4
+// W[16 nt + i16][32 h + 16 q + 4 g + e][t], e = 0..3 (zero past N)
+__global__ void pack_conv2f_kernel(const float* __restrict__ w, float* __restrict__ frag, int N, int ntap) {
+  const int total = 2 * ntap * 2 * 4 * 64 * 4;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int r = i;
+  const int e = r & 3; r >>= 2;
+  const int lane = r & 63; r >>= 6;
+  const int nt = r & 3; r >>= 2;
+  const int c = r;  // (h * ntap + t) * 2 + q
+  const int q = c & 1, ht = c >> 1;
+  const int h = ht / ntap, t = ht - h * ntap;
+  const int co = nt * 16 + (lane & 15);
+  const int ci = 32 * h + 16 * q + 4 * (lane >> 4) + e;
+  frag[i] = co < N ? w[((size_t)co * 64 + ci) * ntap + t] : 0.f;
+}
+
+// ---------------------------------------------------------------------------- //
 // conv1 + ReLU + MaxPool2d(2,2) of cnn-trad-pool2 (1 -> 64 channels, 20 x 8
 // filter, stride 1) in bf16x3, writing conv2x3_kernel's NHWC hi/lo input.
 // One clip per tile, 8 waves = 2 n-groups (out tiles 2ng, 2ng+1) x 4 m-groups.
@@ -633,6 +787,139 @@ __global__ __launch_bounds__(512, 1) void conv1x3_kernel(Conv1X3Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------- //
+// conv1 + ReLU + MaxPool2d(2,2) of cnn-trad-pool2 in fp32 (the conv1x3_kernel
+// design on v_mfma_f32_16x16x4_f32), writing conv2f_kernel's NHWC fp32 input.
+// One clip per tile, 8 waves = 2 n-groups x 4 m-groups.  K = 160 = 10 chunks of
+// 16: lane group g of chunk s holds kh = 2s + (g >> 1), kw = 4 (g & 1) + e for
+// MFMA e = 0..3.  The clip is staged as a "shifted-row" image of 16-B entries,
+// entry (r, c) = x[r][c .. c+3] (c = 0 .. 35), so an operand read is ONE 16-B
+// read feeding 4 MFMAs per out tile; the weights W[co][kh][4 (g & 1) .. +3] are 16
+// contiguous bytes of the OIHW tensor, held in VGPRs for the launch.  M order
+// (pooled pixel, 2x2 member): ReLU, two lane-swap maxes, one 16-B store per lane
+// group.  The next clip's rows load into registers during this clip's MFMAs.
+// ---------------------------------------------------------------------------- //
+constexpr int C1F_COLS = 36;  // entries per image row (the pooled region's 32 columns + kw 0..7 in runs of 4)
+
+struct Conv1FArgs {
+  const float* x;     // [B][H][W]
+  const float* w;     // [64][1][20][8]
+  const float* bias;  // [64]
+  float* out;         // [B][PH][PW][64]
+  int B, H, W, PH, PW;
+};
+
+__global__ __launch_bounds__(512, 1) void conv1f_kernel(Conv1FArgs a) {
+  __shared__ __attribute__((aligned(16))) char img[C1X3_HMAX * C1F_COLS * 16];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ng = wave & 1, mg = wave >> 1;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int nmt = a.PH * a.PW / 4;  // 16-row m-tiles of pooled members (host-checked: PH*PW % 4 == 0)
+  const int clip_floats = a.H * a.W;
+  const int entries = a.H * C1F_COLS;
+
+  f32x4 wf[10][2];
+#pragma unroll
+  for (int s = 0; s < 10; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = (2 * ng + j) * 16 + i16;
+      wf[s][j] = *(const f32x4*)(a.w + ((size_t)co * C1X3_KH + 2 * s + (g >> 1)) * C1X3_KW + 4 * (g & 1));
+    }
+  float bias[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[j][r] = a.bias[(2 * ng + j) * 16 + 4 * g + r];
+
+  // the lane's entry offset at chunk 0 for m-tile mt (chunk s adds 2 rows)
+  auto aoff = [&](int mt) {
+    const int q = 4 * mt + (i16 >> 2), mem = i16 & 3;
+    const int ph = q / a.PW, pw = q - ph * a.PW;
+    const int r = 2 * ph + (mem >> 1) + (g >> 1), c = 2 * pw + (mem & 1) + 4 * (g & 1);
+    return (r * C1F_COLS + c) * 16;
+  };
+  typedef f32x4 BFr[10];
+  auto loadB = [&](BFr& Bv, int off) {
+#pragma unroll
+    for (int s = 0; s < 10; ++s) Bv[s] = *(const f32x4*)(img + off + s * 2 * C1F_COLS * 16);
+  };
+  auto tile = [&](const BFr& Bv, int mt, float* ob) {
+    f32x4 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = f32x4{bias[j][0], bias[j][1], bias[j][2], bias[j][3]};
+#pragma unroll
+    for (int s = 0; s < 10; ++s)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[s][j][e], Bv[s][e], acc[j], 0, 0, 0);
+    const int q = 4 * mt + (i16 >> 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = relu_nan(acc[j][r]);
+        t = nanmax(t, __shfl_xor(t, 1));
+        v[r] = nanmax(t, __shfl_xor(t, 2));
+      }
+      if ((i16 & 3) == 0) *(f32x4*)(ob + (size_t)q * 64 + (2 * ng + j) * 16 + 4 * g) = v;
+    }
+  };
+
+  constexpr int NE = (C1X3_HMAX * C1F_COLS + 511) / 512;
+  f32x4 pu[NE];
+  auto fetch = [&](int bb) {
+    const bool ok = bb < a.B;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.x + (size_t)(ok ? bb : 0) * clip_floats), (short)0, ok ? clip_floats * 4 : 0, 0x00020000);
+#pragma unroll
+    for (int n = 0; n < NE; ++n) {
+      const int e = tid + n * 512;
+      const int r = e / C1F_COLS, c = e - r * C1F_COLS;
+      const int o = e < entries ? (r * a.W + c) * 4 : 0x40000000;
+      pu[n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+    }
+  };
+  fetch(blockIdx.x);
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    __syncthreads();  // every wave is done with the previous clip's image
+#pragma unroll
+    for (int n = 0; n < NE; ++n) {
+      const int e = tid + n * 512;
+      if (e < entries) *(f32x4*)(img + e * 16) = pu[n];
+    }
+    __syncthreads();
+    fetch(b + gridDim.x);  // the next clip's rows, landing during this clip's MFMAs
+    float* ob = a.out + (size_t)b * a.PH * a.PW * 64;
+    BFr B0, B1;
+    int mt = mg;
+    if (mt < nmt) loadB(B0, aoff(mt));
+    while (mt < nmt) {
+      const int m1 = mt + 4;
+      if (m1 < nmt) loadB(B1, aoff(m1));
+      tile(B0, mt, ob);
+      if (m1 >= nmt) break;
+      const int m2 = m1 + 4;
+      if (m2 < nmt) loadB(B0, aoff(m2));
+      tile(B1, m1, ob);
+      mt = m2;
+    }
+  }
+}
+
+// conv1 in fp32 with conv2f following: trad-pool2's conv1 geometry
+static bool conv1f_applies(const honk_cnn_desc* d, int oh1, int ph1, int pw1) {
+  if (const char* e = getenv("HONK_CNN_C1F"))
+    if (atoi(e) == 0) return false;
+  return d->c1_kh == C1X3_KH && d->c1_kw == C1X3_KW && d->c1_sh == 1 && d->c1_sw == 1 && d->c1_out == 64 &&
+         2 * pw1 + 4 <= C1F_COLS && d->width >= C1F_COLS + 3 && d->height <= C1X3_HMAX && (ph1 * pw1) % 4 == 0 &&
+         oh1 >= 2 * ph1;
+}
+
 // conv1 on the fast path: bf16x3 with conv2x3 following, trad-pool2's conv1
 // geometry (20 x 8 filter, stride 1, 64 maps, 2x2 pool, 32 pooled-window columns)
 static bool conv1x3_applies(const honk_cnn_desc* d, int oh1, int ph1, int pw1) {
@@ -657,6 +944,17 @@ static bool conv2x3_applies(const honk_cnn_desc* d, int ph1, int pw1, int oh2, i
          oh2 * ow2 > 16 * C2X3_MT && oh2 * ow2 <= 32 * C2X3_MT;
 }
 static size_t conv2x3_frag_bytes(const honk_cnn_desc* d) { return (size_t)2 * d->c2_kh * d->c2_kw * 4 * 2 * 64 * 16; }
+// the fp32 counterpart (conv2f_kernel): the same geometry in HONK_PREC_F32
+constexpr int C2F_MT = 13;
+static bool conv2f_applies(const honk_cnn_desc* d, int ph1, int pw1, int oh2, int ow2) {
+  if (d->precision != HONK_PREC_F32 || !d->has_conv2) return false;
+  if (const char* e = getenv("HONK_CNN_C2F"))
+    if (atoi(e) == 0) return false;
+  return d->p1_h == 2 && d->p1_w == 2 && d->c1_out == 64 && d->c2_out <= 64 && d->c2_sh == 1 && d->c2_sw == 1 &&
+         d->p2_h == 1 && d->p2_w == 1 && ph1 * pw1 * 128 <= C2X3_IMG && oh2 * ow2 > 16 * C2F_MT &&
+         oh2 * ow2 <= 32 * C2F_MT;
+}
+static size_t conv2f_frag_bytes(const honk_cnn_desc* d) { return (size_t)2 * d->c2_kh * d->c2_kw * 2 * 4 * 64 * 16; }
 
 static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st, bool x3 = false) {
   if (a.M <= 0 || a.N <= 0) return HONK_OK;
@@ -679,7 +977,7 @@ static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st, bool x3 = 
 
 static int conv(const float* in, const float* w, const float* bias, float* out, int64_t batch, int cin,
                 int h, int wd, int cout, int kh, int kw, int sh, int sw, int relu, hipStream_t st,
-                bool pool2 = false, bool x3 = false, bool nhwc_x3 = false) {
+                bool pool2 = false, bool x3 = false, int nhwc_x3 = 0) {
   if (kh > h || kw > wd || sh < 1 || sw < 1 || cin < 1 || cout < 1)
     return fail(HONK_ERR_ARG, "bad conv geometry (cin=%d %dx%d k=%dx%d s=%dx%d)", cin, h, wd, kh, kw, sh, sw);
   GemmArgs a;
@@ -693,7 +991,7 @@ static int conv(const float* in, const float* w, const float* bias, float* out, 
   a.N = cout;
   a.K = cin * kh * kw;
   a.relu = relu;
-  a.nhwc_x3 = nhwc_x3 ? 1 : 0;
+  a.nhwc_x3 = nhwc_x3;
   if (pool2 && (a.PH < 1 || a.PW < 1)) return fail(HONK_ERR_ARG, "pool larger than conv output");
   return launch_gemm(a, pool2, st, x3);
 }
@@ -1223,6 +1521,7 @@ size_t honk_cnn_workspace_bytes(const honk_cnn_desc* d, int64_t batch) {
   if (shapes(d, &s) != HONK_OK || batch < 1) return 0;
   size_t b = (size_t)2 * chunk_clips(s, batch) * per_clip_floats(s) * sizeof(float);
   if (conv2x3_applies(d, s.ph1, s.pw1, s.oh2, s.ow2)) b += conv2x3_frag_bytes(d);  // packed conv2 fragments
+  if (conv2f_applies(d, s.ph1, s.pw1, s.oh2, s.ow2)) b += conv2f_frag_bytes(d);
   return b;
 }
 
@@ -1258,13 +1557,38 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
                        (__bf16*)c2frag, d->c2_out, ntap);
     HONK_LAUNCH_CHECK("pack_conv2x3_kernel");
   }
+  const bool c2f = conv2f_applies(d, s.ph1, s.pw1, s.oh2, s.ow2);
+  if (c2f) {  // conv2 weights -> fp32 fragments (one small launch per call)
+    const int ntap = d->c2_kh * d->c2_kw;
+    const int total = 2 * ntap * 2 * 4 * 64 * 4;
+    hipLaunchKernelGGL(pack_conv2f_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, t[2], (float*)c2frag,
+                       d->c2_out, ntap);
+    HONK_LAUNCH_CHECK("pack_conv2f_kernel");
+  }
 
   for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
     const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
     const float* xin = x + c0 * d->height * d->width;
     // conv1 + ReLU (model.py:187) -> A ; pool1 (:189) -> B (skip when 1x1)
     const bool fuse1 = d->p1_h == 2 && d->p1_w == 2;  // conv1 + ReLU + MaxPool2d(2,2) in one kernel
-    if (c2x3 && conv1x3_applies(d, s.oh1, s.ph1, s.pw1)) {
+    if (c2f && conv1f_applies(d, s.oh1, s.ph1, s.pw1)) {
+      Conv1FArgs c;
+      c.x = xin;
+      c.w = t[0];
+      c.bias = t[1];
+      c.out = A;
+      c.B = (int)n;
+      c.H = d->height;
+      c.W = d->width;
+      c.PH = s.ph1;
+      c.PW = s.pw1;
+      if (n > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
+      const unsigned grid = (unsigned)(n < cu_count() ? n : cu_count());
+      TimedLaunch tl(st, 2.0 * (double)n * s.ph1 * s.pw1 * 4 * 64 * C1X3_KH * C1X3_KW);
+      hipLaunchKernelGGL(conv1f_kernel, dim3(grid), dim3(512), 0, st, c);
+      tl.done(st);
+      HONK_LAUNCH_CHECK("conv1f_kernel");
+    } else if (c2x3 && conv1x3_applies(d, s.oh1, s.ph1, s.pw1)) {
       Conv1X3Args c;
       c.x = xin;
       c.w = t[0];
@@ -1283,7 +1607,7 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
       HONK_LAUNCH_CHECK("conv1x3_kernel");
     } else {
       rc = conv(xin, t[0], t[1], A, n, 1, d->height, d->width, d->c1_out, d->c1_kh, d->c1_kw, d->c1_sh, d->c1_sw, 1,
-                st, fuse1, x3, c2x3);
+                st, fuse1, x3, c2x3 ? 1 : c2f ? 2 : 0);
       if (rc) return rc;
     }
     const float* cur = A;
@@ -1314,6 +1638,28 @@ int honk_cnn_forward(const honk_cnn_desc* d, const float* const* t, const float*
       hipLaunchKernelGGL((conv2x3_kernel<C2X3_MT>), dim3(grid), dim3(256), 0, st, c);
       tl.done(st);
       HONK_LAUNCH_CHECK("conv2x3_kernel");
+      cur = B;
+      other = A;
+    } else if (c2f) {  // model.py:190-193, fp32, on the NHWC pooled conv1 output
+      Conv2FArgs c;
+      c.in = A;
+      c.wfrag = (const f32x4*)c2frag;
+      c.bias = t[3];
+      c.out = B;
+      c.B = (int)n;
+      c.PH = s.ph1;
+      c.PW = s.pw1;
+      c.KW = d->c2_kw;
+      c.ntap = d->c2_kh * d->c2_kw;
+      c.OH = s.oh2;
+      c.OW = s.ow2;
+      c.N = d->c2_out;
+      if (n > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
+      const unsigned grid = (unsigned)(n < cu_count() ? n : cu_count());
+      TimedLaunch tl(st, 2.0 * (double)n * s.oh2 * s.ow2 * d->c2_out * 64 * c.ntap);
+      hipLaunchKernelGGL((conv2f_kernel<C2F_MT>), dim3(grid), dim3(256), 0, st, c);
+      tl.done(st);
+      HONK_LAUNCH_CHECK("conv2f_kernel");
       cur = B;
       other = A;
     } else if (d->has_conv2) {  // model.py:190-193
