@@ -61,6 +61,11 @@ _PROTOS = {
     "honk_conv2d_dgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64] + [ctypes.c_int32] * 6),
     "honk_conv2d_dgrad_f32": (ctypes.c_int, [c_f32p] * 4 + [ctypes.c_int64] + [ctypes.c_int32] * 6
                               + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_conv_same_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64] + [ctypes.c_int32] * 4),
+    "honk_conv_same_f32": (ctypes.c_int, [c_f32p] * 3 + [ctypes.c_int64] + [ctypes.c_int32] * 5
+                           + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_conv_same_wgrad_f32": (ctypes.c_int, [c_f32p] * 3 + [ctypes.c_int64] + [ctypes.c_int32] * 4
+                                 + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "honk_sgd_step_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64, ctypes.c_float, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p]),
     "honk_conv3x3_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 5

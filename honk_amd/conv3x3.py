@@ -4,7 +4,9 @@
 of SpeechResModel's block stack (/root/reference/utils/model.py:94-98: d = 1 for
 res8/res26 and -narrow, d = 2**(i//3) for res15 and res15-narrow) as an autograd
 function whose forward, input gradient and weight gradient are
-``honk_conv3x3_f32`` / ``honk_conv3x3_wgrad_f32``;
+``honk_conv3x3_f32`` / ``honk_conv3x3_wgrad_f32`` (the dedicated 19- and 45-map
+kernels) or, for any other ``n_feature_maps`` a ConfigBuilder flag may set
+(utils/train.py:21-33), ``honk_conv_same_f32`` / ``honk_conv_same_wgrad_f32``;
 ``batch_norm_train(x, bn)`` is the blocks' train-mode ``BatchNorm2d(affine=False)``
 (model.py:100, 117-118) on ``honk_bn_train_fwd/bwd_f32``; ``res_tail`` fuses a
 block's relu, residual add and that BatchNorm (``honk_res_tail_fwd/bwd_f32``) and
@@ -22,16 +24,25 @@ CHANNELS = (19, 45)
 
 
 def supported(x, conv) -> bool:
-    """The native kernels cover bias-free 3x3 convs with padding == dilation (the res
-    blocks' "same" convs) whose (C, H, W, dilation) the library accepts
-    (honk_conv3x3_check, host-only: C in CHANNELS, the band plan fits)."""
+    """The native kernels cover bias-free C -> C 3x3 convs with padding == dilation (the
+    res blocks' "same" convs) for any C: the dedicated {19, 45}-map kernels where the
+    library accepts the shape (honk_conv3x3_check, host-only), the general same-conv
+    path (honk_conv_same_f32: zero-padded input + implicit GEMM) otherwise."""
     d = tuple(conv.dilation)
-    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.weight.shape[0] in CHANNELS
-            and tuple(conv.kernel_size) == (3, 3) and d[0] == d[1] and 1 <= d[0] <= 64
-            and tuple(conv.padding) == d and tuple(conv.stride) == (1, 1) and conv.bias is None):
-        return False
-    return _native.load().honk_conv3x3_check(int(conv.weight.shape[0]), int(x.shape[2]), int(x.shape[3]),
-                                             int(d[0])) == 0
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.in_channels == conv.out_channels
+            and x.shape[1] == conv.in_channels and tuple(conv.kernel_size) == (3, 3) and d[0] == d[1]
+            and 1 <= d[0] <= 1024 and tuple(conv.padding) == d and tuple(conv.stride) == (1, 1)
+            and conv.bias is None and conv.groups == 1)
+
+
+def _dedicated(C, H, W, d) -> bool:
+    """The {19, 45}-map kernels take (C, H, W, d) (host-only query)."""
+    return C in CHANNELS and _native.load().honk_conv3x3_check(int(C), int(H), int(W), int(d)) == 0
+
+
+def _same_ws(B, C, H, W, d, device):
+    n = int(_native.load().honk_conv_same_workspace_bytes(B, C, H, W, d))
+    return torch.empty(max(n, 1), dtype=torch.uint8, device=device), n
 
 
 _warned = set()
@@ -53,9 +64,14 @@ def _conv(x, w, flip, d=1):
     x = x.contiguous()
     B, C, H, W = x.shape
     y = torch.empty_like(x)
-    _native.check(_native.load().honk_conv3x3_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W, d,
-                                                  1 if flip else 0, _native.stream_handle(x.device)),
-                  "honk_conv3x3_f32")
+    lib = _native.load()
+    if _dedicated(C, H, W, d):
+        _native.check(lib.honk_conv3x3_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W, d, 1 if flip else 0,
+                                           _native.stream_handle(x.device)), "honk_conv3x3_f32")
+        return y
+    ws, nb = _same_ws(B, C, H, W, d, x.device)
+    _native.check(lib.honk_conv_same_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W, d, 1 if flip else 0,
+                                         ws.data_ptr(), nb, _native.stream_handle(x.device)), "honk_conv_same_f32")
     return y
 
 
@@ -64,11 +80,17 @@ def _wgrad(x, dy, d=1):
     B, C, H, W = x.shape
     lib = _native.load()
     dw = torch.empty(C, C, 3, 3, dtype=torch.float32, device=x.device)
-    nbytes = lib.honk_conv3x3_wgrad_workspace_bytes(B, C, H, W, d)
-    ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=x.device)
-    _native.check(lib.honk_conv3x3_wgrad_f32(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), B, C, H, W, d,
-                                             ws.data_ptr(), nbytes, _native.stream_handle(x.device)),
-                  "honk_conv3x3_wgrad_f32")
+    if _dedicated(C, H, W, d):
+        nbytes = lib.honk_conv3x3_wgrad_workspace_bytes(B, C, H, W, d)
+        ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=x.device)
+        _native.check(lib.honk_conv3x3_wgrad_f32(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), B, C, H, W, d,
+                                                 ws.data_ptr(), nbytes, _native.stream_handle(x.device)),
+                      "honk_conv3x3_wgrad_f32")
+        return dw
+    ws, nb = _same_ws(B, C, H, W, d, x.device)
+    _native.check(lib.honk_conv_same_wgrad_f32(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), B, C, H, W, d,
+                                               ws.data_ptr(), nb, _native.stream_handle(x.device)),
+                  "honk_conv_same_wgrad_f32")
     return dw
 
 

@@ -31,6 +31,7 @@ struct GemmArgs {
   int64_t M;         // GEMM rows: B*OH*OW, or B*PH*PW*4 (pool2: 4 window members per pooled pixel)
   int N, K;
   int Cin, H, W, KH, KW, SH, SW, OH, OW;
+  int DH, DW;        // dilation (1: the SpeechModel convs; the res block convs of honk_conv_same_f32)
   int PH, PW;        // pooled output dims (pool2 fused)
   int relu;
   int nhwc_x3;       // POOL2 only: 1 = store [B][PH][PW][hi N | lo N] bf16 (conv2x3_kernel's input),
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
     for (int k = tid; k < a.K; k += 256) {
       const int ci = k / KHW, rem = k - ci * KHW;
       const int kh = rem / a.KW, kw = rem - kh * a.KW;
-      ktab[k] = (ci * a.H + kh) * a.W + kw;
+      ktab[k] = (ci * a.H + kh * a.DH) * a.W + kw * a.DW;
     }
 
   // X staging: thread owns pixel column mm = tid % 128 and rows kk = tid/128 + 2r
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a) {
     if (use_tab) return ktab[k];
     const int ci = k / KHW, rem = k - ci * KHW;
     const int kh = rem / a.KW, kw = rem - kh * a.KW;
-    return (ci * a.H + kh) * a.W + kw;
+    return (ci * a.H + kh * a.DH) * a.W + kw * a.DW;
   };
   auto load_slice = [&](int k0) {
 #pragma unroll
@@ -977,14 +978,15 @@ static int launch_gemm(const GemmArgs& a, bool pool2, hipStream_t st, bool x3 = 
 
 static int conv(const float* in, const float* w, const float* bias, float* out, int64_t batch, int cin,
                 int h, int wd, int cout, int kh, int kw, int sh, int sw, int relu, hipStream_t st,
-                bool pool2 = false, bool x3 = false, int nhwc_x3 = 0) {
-  if (kh > h || kw > wd || sh < 1 || sw < 1 || cin < 1 || cout < 1)
+                bool pool2 = false, bool x3 = false, int nhwc_x3 = 0, int dil = 1) {
+  if ((kh - 1) * dil + 1 > h || (kw - 1) * dil + 1 > wd || sh < 1 || sw < 1 || cin < 1 || cout < 1 || dil < 1)
     return fail(HONK_ERR_ARG, "bad conv geometry (cin=%d %dx%d k=%dx%d s=%dx%d)", cin, h, wd, kh, kw, sh, sw);
   GemmArgs a;
   a.in = in; a.w = w; a.bias = bias; a.out = out;
   a.Cin = cin; a.H = h; a.W = wd; a.KH = kh; a.KW = kw; a.SH = sh; a.SW = sw;
-  a.OH = (h - kh) / sh + 1;
-  a.OW = (wd - kw) / sw + 1;
+  a.DH = a.DW = dil;
+  a.OH = (h - (kh - 1) * dil - 1) / sh + 1;
+  a.OW = (wd - (kw - 1) * dil - 1) / sw + 1;
   a.PH = a.OH / 2;
   a.PW = a.OW / 2;
   a.M = pool2 ? batch * a.PH * a.PW * 4 : batch * a.OH * a.OW;
@@ -1151,6 +1153,7 @@ struct ConvWgradArgs {
   float* pbias;      // [S][N] or nullptr
   int64_t M, mper;   // B*OH*OW; m per split (multiple of WG_BM)
   int N, K, Cin, H, W, KH, KW, SH, SW, OH, OW;
+  int D;             // dilation
 };
 
 // 256 threads = 4 waves; wave w owns out channels n0 + 16w .. +15 and all 4
@@ -1174,7 +1177,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
     if (k < a.K) {
       const int ci = k / KHW, rem = k - ci * KHW;
       const int kh = rem / a.KW, kw = rem - kh * a.KW;
-      koff[j] = (ci * a.H + kh) * a.W + kw;
+      koff[j] = (ci * a.H + kh * a.D) * a.W + kw * a.D;
     } else {
       koff[j] = -1;
     }
@@ -1313,9 +1316,10 @@ struct WgradPlanC {
   int tn, tk, S;
   int64_t M, mper;
 };
-static WgradPlanC wgrad_plan_c(int64_t batch, int cin, int h, int w, int cout, int kh, int kw, int sh, int sw) {
+static WgradPlanC wgrad_plan_c(int64_t batch, int cin, int h, int w, int cout, int kh, int kw, int sh, int sw,
+                               int dil = 1) {
   WgradPlanC p;
-  const int oh = (h - kh) / sh + 1, ow = (w - kw) / sw + 1;
+  const int oh = (h - (kh - 1) * dil - 1) / sh + 1, ow = (w - (kw - 1) * dil - 1) / sw + 1;
   p.M = batch * oh * ow;
   p.tn = (int)cdiv(cout, WG_BN);
   p.tk = (int)cdiv((int64_t)cin * kh * kw, WG_BK);
@@ -1328,6 +1332,58 @@ static WgradPlanC wgrad_plan_c(int64_t batch, int cin, int h, int w, int cout, i
   p.S = (int)cdiv(p.M, p.mper);
   if (p.S < 1) p.S = 1;
   return p;
+}
+
+
+// the weight / bias gradient launches (conv_wgrad_kernel + the fixed-order split sums)
+static int wgrad_launch(const float* in, const float* gy, const float* act, float* dw, float* db, int64_t batch,
+                        int cin, int h, int w, int cout, int kh, int kw, int sh, int sw, int dil, float* part,
+                        hipStream_t st) {
+  const int64_t K = (int64_t)cin * kh * kw;
+  const WgradPlanC p = wgrad_plan_c(batch, cin, h, w, cout, kh, kw, sh, sw, dil);
+  ConvWgradArgs a;
+  a.in = in; a.gy = gy; a.act = act;
+  a.part = part;
+  a.pbias = db ? a.part + (int64_t)p.S * cout * K : nullptr;
+  a.M = p.M; a.mper = p.mper;
+  a.N = cout; a.K = (int)K; a.Cin = cin; a.H = h; a.W = w; a.KH = kh; a.KW = kw; a.SH = sh; a.SW = sw;
+  a.OH = (h - (kh - 1) * dil - 1) / sh + 1; a.OW = (w - (kw - 1) * dil - 1) / sw + 1;
+  a.D = dil;
+  {
+    TimedLaunch tl(st, 2.0 * (double)p.M * cout * K);
+    hipLaunchKernelGGL(conv_wgrad_kernel, dim3(p.tn, p.tk, p.S), dim3(256), 0, st, a);
+    tl.done(st);
+  }
+  HONK_LAUNCH_CHECK("conv_wgrad_kernel");
+  const int64_t nw = (int64_t)cout * K;
+  hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)cdiv(nw, 256)), dim3(256), 0, st, a.part, dw, nw, p.S);
+  if (db)
+    hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)cdiv(cout, 256)), dim3(256), 0, st, a.pbias, db,
+                       (int64_t)cout, p.S);
+  HONK_LAUNCH_CHECK("split_sum_kernel");
+  return HONK_OK;
+}
+
+// xp[pl][y][x] = x[pl][y - d][x - d] inside the map, else 0 (the "same" conv's zero padding)
+__global__ __launch_bounds__(256) void pad_same_kernel(const float* __restrict__ x, float* __restrict__ xp,
+                                                       int64_t planes, int H, int W, int d) {
+  const int Hp = H + 2 * d, Wp = W + 2 * d;
+  const int64_t total = planes * Hp * Wp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int xx = (int)(i % Wp);
+    const int64_t t = i / Wp;
+    const int yy = (int)(t % Hp);
+    const int64_t pl = t / Hp;
+    const int sy = yy - d, sx = xx - d;
+    xp[i] = (sy >= 0 && sy < H && sx >= 0 && sx < W) ? x[(pl * H + sy) * W + sx] : 0.f;
+  }
+}
+static int pad_same(const float* x, float* xp, int64_t planes, int h, int w, int d, hipStream_t st) {
+  const int64_t total = planes * (int64_t)(h + 2 * d) * (w + 2 * d);
+  const int64_t blocks = cdiv(total, 256) < 65536 ? cdiv(total, 256) : 65536;
+  hipLaunchKernelGGL(pad_same_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, xp, planes, h, w, d);
+  HONK_LAUNCH_CHECK("pad_same_kernel");
+  return HONK_OK;
 }
 
 struct Shapes {
@@ -1460,27 +1516,7 @@ int honk_conv2d_wgrad_f32(const float* in, const float* gy, const float* act, fl
   }
   const size_t need = honk_conv2d_wgrad_workspace_bytes(batch, cin, h, w, cout, kh, kw, sh, sw);
   if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
-  const WgradPlanC p = wgrad_plan_c(batch, cin, h, w, cout, kh, kw, sh, sw);
-  ConvWgradArgs a;
-  a.in = in; a.gy = gy; a.act = act;
-  a.part = (float*)workspace;
-  a.pbias = db ? a.part + (int64_t)p.S * cout * K : nullptr;
-  a.M = p.M; a.mper = p.mper;
-  a.N = cout; a.K = (int)K; a.Cin = cin; a.H = h; a.W = w; a.KH = kh; a.KW = kw; a.SH = sh; a.SW = sw;
-  a.OH = (h - kh) / sh + 1; a.OW = (w - kw) / sw + 1;
-  {
-    TimedLaunch tl(st, 2.0 * (double)p.M * cout * K);
-    hipLaunchKernelGGL(conv_wgrad_kernel, dim3(p.tn, p.tk, p.S), dim3(256), 0, st, a);
-    tl.done(st);
-  }
-  HONK_LAUNCH_CHECK("conv_wgrad_kernel");
-  const int64_t nw = (int64_t)cout * K;
-  hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)cdiv(nw, 256)), dim3(256), 0, st, a.part, dw, nw, p.S);
-  if (db)
-    hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)cdiv(cout, 256)), dim3(256), 0, st, a.pbias, db,
-                       (int64_t)cout, p.S);
-  HONK_LAUNCH_CHECK("split_sum_kernel");
-  return HONK_OK;
+  return wgrad_launch(in, gy, act, dw, db, batch, cin, h, w, cout, kh, kw, sh, sw, 1, (float*)workspace, st);
 }
 
 size_t honk_conv2d_dgrad_workspace_bytes(int64_t batch, int32_t cin, int32_t h, int32_t w, int32_t cout, int32_t kh,
@@ -1514,6 +1550,70 @@ int honk_conv2d_dgrad_f32(const float* gy, const float* act, const float* w, flo
   hipLaunchKernelGGL(flip_weights_kernel, dim3((unsigned)cdiv(nw, 256)), dim3(256), 0, st, w, wf, cout, cin, kh, kw);
   HONK_LAUNCH_CHECK("flip_weights_kernel");
   return conv(gp, wf, nullptr, dx, batch, cout, php, pwp, cin, kh, kw, 1, 1, 0, st);
+}
+
+// ---- the res block conv for any channel count (model.py:94-98: 3x3, padding =
+// dilation = d, no bias), the training kernels' general path: the input zero-padded
+// into the workspace, then the implicit GEMM with dilation ----
+static int same_check(const void* a, const void* b, const void* c, int64_t batch, int32_t ch, int32_t h, int32_t w,
+                      int32_t d) {
+  if (!a || !b || !c) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 0 || ch < 1 || h < 1 || w < 1 || d < 1 || d > 1024)
+    return fail(HONK_ERR_ARG, "bad same-conv shape (B=%lld C=%d H=%d W=%d d=%d)", (long long)batch, ch, h, w, d);
+  if ((int64_t)ch * 9 > 0x7fffffff / 4) return fail(HONK_ERR_UNSUPPORTED, "same-conv: C=%d too large", ch);
+  return HONK_OK;
+}
+
+size_t honk_conv_same_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil) {
+  if (batch < 1 || c < 1 || h < 1 || w_ < 1 || dil < 1) return 0;
+  const int hp = h + 2 * dil, wp = w_ + 2 * dil;
+  const size_t pad = (size_t)batch * c * hp * wp;
+  const WgradPlanC p = wgrad_plan_c(batch, c, hp, wp, c, 3, 3, 1, 1, dil);
+  size_t extra = (size_t)p.S * c * c * 9;
+  if ((size_t)c * c * 9 > extra) extra = (size_t)c * c * 9;
+  return (pad + extra) * sizeof(float);
+}
+
+int honk_conv_same_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h, int32_t w_,
+                       int32_t dil, int32_t flip, void* workspace, size_t ws_bytes, void* stream) {
+  int rc = same_check(x, w, y, batch, c, h, w_, dil);
+  if (rc) return rc;
+  if (batch == 0) return HONK_OK;
+  const size_t need = honk_conv_same_workspace_bytes(batch, c, h, w_, dil);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  const int hp = h + 2 * dil, wp = w_ + 2 * dil;
+  float* xp = (float*)workspace;
+  float* wf = xp + (size_t)batch * c * hp * wp;
+  rc = pad_same(x, xp, batch * c, h, w_, dil, st);
+  if (rc) return rc;
+  const float* wk = w;
+  if (flip) {  // input gradient: the flipped, transposed kernel, w'[i][o][t] = w[o][i][8 - t]
+    const int64_t nw = (int64_t)c * c * 9;
+    hipLaunchKernelGGL(flip_weights_kernel, dim3((unsigned)cdiv(nw, 256)), dim3(256), 0, st, w, wf, c, c, 3, 3);
+    HONK_LAUNCH_CHECK("flip_weights_kernel");
+    wk = wf;
+  }
+  return conv(xp, wk, nullptr, y, batch, c, hp, wp, c, 3, 3, 1, 1, 0, st, false, false, 0, dil);
+}
+
+int honk_conv_same_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c, int32_t h,
+                             int32_t w_, int32_t dil, void* workspace, size_t ws_bytes, void* stream) {
+  int rc = same_check(x, dy, dw, batch, c, h, w_, dil);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (batch == 0) {
+    HONK_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)c * c * 9 * sizeof(float), st));
+    return HONK_OK;
+  }
+  const size_t need = honk_conv_same_workspace_bytes(batch, c, h, w_, dil);
+  if (!workspace || ws_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
+  const int hp = h + 2 * dil, wp = w_ + 2 * dil;
+  float* xp = (float*)workspace;
+  float* part = xp + (size_t)batch * c * hp * wp;
+  rc = pad_same(x, xp, batch * c, h, w_, dil, st);
+  if (rc) return rc;
+  return wgrad_launch(xp, dy, nullptr, dw, nullptr, batch, c, hp, wp, c, 3, 3, 1, 1, dil, part, st);
 }
 
 size_t honk_cnn_workspace_bytes(const honk_cnn_desc* d, int64_t batch) {

@@ -158,6 +158,20 @@ int honk_conv2d_dgrad_f32(const float* gy, const float* act, const float* w, flo
                           int32_t h, int32_t w_, int32_t cout, int32_t kh, int32_t kw, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/*
+ * The res block conv for ANY channel count C (3x3, padding = dilation = dil, no bias,
+ * NCHW fp32; model.py:94-98) -- the general path under honk_conv3x3_f32's
+ * {19, 45}-map kernels: the input zero-padded into the workspace, then the fp32-MFMA
+ * implicit GEMM with dilation.  flip = 1: the input gradient (w'[i][o][t] =
+ * w[o][i][8-t], as honk_conv3x3_f32).  The weight gradient as
+ * honk_conv3x3_wgrad_f32 (deterministic).  Workspace: honk_conv_same_workspace_bytes.
+ */
+size_t honk_conv_same_workspace_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil);
+int honk_conv_same_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h, int32_t w_,
+                       int32_t dil, int32_t flip, void* workspace, size_t workspace_bytes, void* stream);
+int honk_conv_same_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c, int32_t h,
+                             int32_t w_, int32_t dil, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- MFCC front-end (AudioPreprocessor.compute_mfccs, utils/manage_audio.py:30-42) ---- */
 /*
  * pcm [batch][samples] f32 -> out [batch][1 + samples/hop][n_dct] f32 (the
