@@ -750,6 +750,7 @@ static int bands_w(const Layout& L, const honk_res_desc* d, int SP, int i) {
 struct PairPlan {
   bool ok;
   int lag, NRA, NRB, slotb, ppr, ppw;  // ppw: DMA pieces per A wave per step
+  int ns;                              // streams per workgroup (block16p_kernel NS)
 };
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t n, int grid, int i);
 static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
@@ -773,8 +774,8 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
 // Fused pair plan (res_bf16p.inc) for layers A (dilation d) and B (tap stride sB
 // class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
-static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw) {
-  PairPlan pp{false, 0, 0, 0, 0, 0, 0};
+static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw, int nstreams = 1) {
+  PairPlan pp{false, 0, 0, 0, 0, 0, 0, nstreams};
   const int P = 64, W = L.W, H = L.H;
   const long PXB = g16p_pxb(L.NT, SP);  // LDS pixel pitch
   pp.ppr = (int)((W * PXB + 1023) / 1024);
@@ -837,7 +838,7 @@ static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw) {
   if (F(-1) < 0) return pp;
   pp.NRA = (int)(nra > 2 ? nra : 2);
   pp.NRB = (int)(nrb > 2 ? nrb : 2);
-  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + 256 + 1024 <= g16p_lds_bytes();
+  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + 256 + 1024 <= g16p_lds_bytes() / nstreams;
   return pp;
 }
 
@@ -852,7 +853,7 @@ static int pair_ppw(int SP, int ppr) {
   return ppr == 4 ? 4 : ppr == 2 ? 5 : 0;
 }
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t n, int grid, int i) {
-  const PairPlan no{false, 0, 0, 0, 0, 0, 0};
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 1};
   const char* kenv = getenv("HONK_RES_KERNEL");
   if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
   if (i % 2 == 0 || i + 1 >= L.L) return no;
@@ -860,6 +861,12 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t
   const int sB = dB == dA ? 1 : (dB == 2 * dA ? 2 : 0);
   const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
   if (!sB || cb >= 0xE0000000ull) return no;
+  // bf16 with full 40-pixel rows: two streams per workgroup when both rings fit half the LDS
+  const char* nse = getenv("HONK_PAIR_STREAMS");
+  if (SP == 1 && !(nse && nse[0] == '1')) {
+    const PairPlan p2 = plan_pair(L, SP, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2);
+    if (p2.ok && p2.ppr == 4 && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
+  }
   const PairPlan pp = plan_pair(L, SP, dA, sB, (int)cdiv(n, grid));
   const int ppw = pair_ppw(SP, pp.ppr);
   return pp.ok && ppw && pp.ppw <= ppw ? pp : no;
@@ -1024,12 +1031,13 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.slotb = pp.slotb;
             pa.ppr = pp.ppr;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
-            const dim3 gd(grid), bd(256);
-            if (SP == 2 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9>), gd, bd, 0, st, pa);
-            else if (SP == 2 && pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10>), gd, bd, 0, st, pa);
-            else if (SP == 2) hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9>), gd, bd, 0, st, pa);
-            else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4>), gd, bd, 0, st, pa);
-            else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5>), gd, bd, 0, st, pa);
+            const dim3 gd(grid), bd(256 * pp.ns);
+            if (SP == 2 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9, 1>), gd, bd, 0, st, pa);
+            else if (SP == 2 && pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10, 1>), gd, bd, 0, st, pa);
+            else if (SP == 2) hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9, 1>), gd, bd, 0, st, pa);
+            else if (pp.ppr == 4 && pp.ns == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
+            else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1>), gd, bd, 0, st, pa);
+            else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 1>), gd, bd, 0, st, pa);
             HONK_LAUNCH_CHECK("res block16p_kernel");
             tl.done(st);
             ++i;  // layer i + 1 done too
