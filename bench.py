@@ -436,7 +436,8 @@ def measure_c2(ctx, args):
             "roofline": {"bound": "mfma",
                          "kernel": ("honk::cnn::conv1x3_kernel + conv2x3_kernel (bf16x3 convs, 3 bf16 MFMA "
                                     "products per MAC; peak = bf16 peak / 3)" if prec == "bf16x3" else
-                                    "honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM convs, fp32 MFMA)"),
+                                    "honk::cnn::conv1f_kernel + conv2f_kernel (fused conv1+ReLU+max-pool and whole-clip conv2, "
+                                    "fp32 MFMA 16x16x4)"),
                          "achieved": round(ach, 2) if ach else None, "peak": round(peak, 1), "unit": "TFLOP/s",
                          "frac": round(ach / peak, 4) if ach else None, "launches": nl,
                          "avg_launch_ms": round(kms / max(nl, 1), 4), "flop_per_launch": kfl / max(nl, 1),
@@ -615,7 +616,8 @@ def rank_main(args):
         avg_ms = kms / max(nlaunch, 1)
         ach = (kflop / max(nlaunch, 1)) / (avg_ms * 1e-3) / 1e12 if nlaunch else None
         roof = {"bound": "mfma",
-                "kernel": ("honk::cnn::conv_gemm_kernel<.., X3=false> (implicit-GEMM conv/linear, fp32 MFMA)"
+                "kernel": ("honk::cnn conv kernels in fp32 (conv1f_kernel + conv2f_kernel where the shapes fit, "
+                           "else conv_gemm_kernel implicit GEMM; fp32 MFMA)"
                            if prec == "f32" else
                            "honk::cnn conv kernels in bf16x3 (3 bf16 MFMA products per MAC; peak = bf16 peak / 3)"),
                 "achieved": round(ach, 2) if ach else None, "peak": round(MODE_PEAK[prec], 1), "unit": "TFLOP/s",

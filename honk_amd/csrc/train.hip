@@ -402,33 +402,69 @@ __host__ __device__ inline TdGeo td_geo(int C, int W, int TH) {
   return g;
 }
 
+// The 16x16x4 MFMA puts output channels 0..15 on one tile; channels 16..C-1 (C <= 20)
+// run on v_mfma_f32_4x4x1_16b_f32 (16 blocks of 4 x 4): the weight of one k for 4
+// channels is broadcast to all 16 blocks (CBSZ = 4, ABID = the source block), each
+// block takes 4 of the 64 pixels of a super tile.  19 channels: 16 + 4 rows instead
+// of 2 x 16 (0.95 instead of 0.59 of the MFMA rows do work).  The 4x4 operand (one
+// k, 64 pixels per register) is the 16x16x4 operands (4 k x 16 pixels, four
+// registers for 64 pixels) transposed by 16-lane rows: two permlane32 and two
+// permlane16 swaps.  Both accumulate k = 9 c + t in ascending order, one fmaf per k
+// (the VALU kernel's chain): bit-identical to it.
+__device__ __forceinline__ void tr4_rows(float& x0, float& x1, float& x2, float& x3) {
+  // on exit 16-lane row g of x_q holds row q of x_g (on entry)
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x0), __float_as_uint(x2), false, false);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x1), __float_as_uint(x3), false, false);
+  const auto r = __builtin_amdgcn_permlane16_swap(p[0], q[0], false, false);
+  const auto u = __builtin_amdgcn_permlane16_swap(p[1], q[1], false, false);
+  x0 = __uint_as_float(r[0]);
+  x1 = __uint_as_float(r[1]);
+  x2 = __uint_as_float(u[0]);
+  x3 = __uint_as_float(u[1]);
+}
+
+// acc += A(block abid, broadcast to all 16 blocks) x b, abid a constant after unrolling
+__device__ __forceinline__ f32x4_t mfma4_bc(float a, float b, f32x4_t c, int abid) {
+  switch (abid & 15) {
+#define HONK_MF4(i) \
+  case i:           \
+    return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 4, i, 0);
+    HONK_MF4(0) HONK_MF4(1) HONK_MF4(2) HONK_MF4(3) HONK_MF4(4) HONK_MF4(5) HONK_MF4(6) HONK_MF4(7)
+    HONK_MF4(8) HONK_MF4(9) HONK_MF4(10) HONK_MF4(11) HONK_MF4(12) HONK_MF4(13) HONK_MF4(14)
+    default: return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 4, 15, 0);
+#undef HONK_MF4
+  }
+}
+
 template <int C>
 __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
-  static_assert(C <= 20, "conv3x3d_kernel: C <= 20");
-  constexpr int K = 9 * C, KS = (K + 3) / 4;
+  static_assert(C > 16 && C <= 20, "conv3x3d_kernel: 16 < C <= 20");
+  constexpr int K = 9 * C, KS = (K + 3) / 4, KT = (K + 15) / 16;
   __shared__ __attribute__((aligned(16))) float tdl[2 * TD_BUF / 4];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i16 = lane & 15, kk = lane >> 4;
   const int d = a.g.d, W = a.W, H = a.H;
   const TdGeo G = td_geo(C, W, a.g.TH);
-  float wr[KS][2];
+  auto wv = [&](int o, int k) -> float {  // the layer weight of output o, k = 9 c + t
+    if (o >= C || k >= K) return 0.f;
+    const int c = k / 9, t = k - 9 * c;
+    return a.flip ? a.w[(c * C + o) * 9 + 8 - t] : a.w[(o * C + c) * 9 + t];
+  };
+  float wr[KS];  // 16x16x4 A operand: lane (kk, i16) = w[i16][4 s + kk]
+  float wt[KT];  // 4x4 A operand: lane 4 b + r = w[16 + r][16 j + b]
   unsigned koff[(KS + 1) / 2];
 #pragma unroll
   for (int s = 0; s < (KS + 1) / 2; ++s) koff[s] = 0;
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int k = 4 * s + kk, c = k / 9, t = k - 9 * c;
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int o = 16 * n + i16;
-      float v = 0.f;
-      if (o < C && k < K) v = a.flip ? a.w[(c * C + o) * 9 + 8 - t] : a.w[(o * C + c) * 9 + t];
-      wr[s][n] = v;
-    }
+    wr[s] = wv(i16, k);
     const unsigned off = k < K ? (unsigned)(c * G.PS + (t / 3) * G.Wr + (t % 3) * d) : 0u;
     koff[s >> 1] |= off << (16 * (s & 1));
   }
+#pragma unroll
+  for (int j = 0; j < KT; ++j) wt[j] = wv(16 + (lane & 3), 16 * j + (lane >> 2));
   // per lane and DMA instruction i: chunk e = (wave TD_ITER + i) 64 + lane of the
   // buffer -> (plane c, row rr, 16-B column cc); tile-invariant byte offset of the
   // chunk in its clip (row 0), or -1 for a zero chunk
@@ -473,29 +509,54 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
     const int b = tile / a.g.nband;
     int r, k0, th;
     band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
-    const int npx = th * W, nmt = (npx + 15) >> 4;
+    const int npx = th * W, nst = (npx + 63) >> 6;
     float* yb = a.y + (size_t)b * clip;
-    for (int m = wave; m < nmt; m += 8) {
-      const int p = 16 * m + i16;
-      const bool pv = p < npx;
-      const int j = pv ? p / W : 0, col = pv ? p - j * W : 0;
-      const float* xp = cur + j * G.Wr + col + TD_PAD - d;
-      f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+    for (int m = wave; m < nst; m += 8) {  // super tile m: pixels 64 m .. 64 m + 63 of the band
+      int xo[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int p = 64 * m + 16 * g + i16;
+        const int pp = p < npx ? p : 0, j = pp / W, col = pp - j * W;
+        xo[g] = j * G.Wr + col + TD_PAD - d;
+      }
+      f32x4_t acc[4], acc4 = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      auto kof = [&](int s) { return (int)((koff[s >> 1] >> (16 * (s & 1))) & 0xffffu); };
+      float xv[4];  // the operands of k-step s; those of s + 1 are read before s's MFMAs
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xv[g] = cur[xo[g] + kof(0)];
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const float xv = xp[(koff[s >> 1] >> (16 * (s & 1))) & 0xffffu];
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s][0], xv, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s][1], xv, acc[1], 0, 0, 0);
+        float xn[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xn[g] = s + 1 < KS ? cur[xo[g] + kof(s + 1)] : 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s], xv[g], acc[g], 0, 0, 0);
+        tr4_rows(xv[0], xv[1], xv[2], xv[3]);  // xv[q] lane l = x(k = 4 s + q, pixel 64 m + l)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (4 * s + q < K) acc4 = mfma4_bc(wt[(4 * s + q) >> 4], xv[q], acc4, 4 * s + q);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xv[g] = xn[g];
       }
-      if (pv) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int p = 64 * m + 16 * g + i16;
+        if (p < npx) {
+          const int j = p / W, col = p - j * W;
+          const size_t pix = (size_t)(r + (k0 + j) * d) * W + col;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) yb[(size_t)(4 * kk + i) * H * W + pix] = acc[g][i];
+        }
+      }
+      const int p = 64 * m + lane;
+      if (p < npx) {
+        const int j = p / W, col = p - j * W;
         const size_t pix = (size_t)(r + (k0 + j) * d) * W + col;
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int o = 16 * n + 4 * kk + i;
-            if (o < C) yb[(size_t)o * H * W + pix] = acc[n][i];
-          }
+        for (int i = 0; i < 4; ++i)
+          if (16 + i < C) yb[(size_t)(16 + i) * H * W + pix] = acc4[i];
       }
     }
   }
@@ -802,8 +863,8 @@ __host__ __device__ inline int twd_nchunk(int C, int W, int TH) {
 
 template <int C>
 __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
-  static_assert(C <= 20, "wgrad3x3d_kernel: C <= 20");
-  constexpr int K9 = 9 * C, NJ = (K9 + 15) / 16, NO = (C + 15) / 16;
+  static_assert(C > 16 && C <= 20, "wgrad3x3d_kernel: 16 < C <= 20");
+  constexpr int K9 = 9 * C, NJ = (K9 + 15) / 16, NH = (K9 + 63) / 64;
   __shared__ __attribute__((aligned(16))) float tdl[2 * TWD_BUF / 4];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -818,11 +879,14 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
     const int j = 16 * n + i16, ci = j / 9, t = j - 9 * ci;
     joff[n] = j < K9 ? ci * G.PS + (t / 3) * G.Wr + (t % 3) * d : 0;
   }
-  f32x4_t acc[NO][NJ];
+  // outputs 0..15: 16x16x4 tiles acc[n] (rows o, columns j = 16 n + i16); outputs 16..C-1:
+  // 4x4x1 blocks acc4[h] (block b, column c: j = 64 h + 4 b + c), the dy of one pixel
+  // for 4 outputs broadcast from block 4 q (conv3x3d_kernel's scheme)
+  f32x4_t acc[NJ], acc4[NH];
 #pragma unroll
-  for (int m = 0; m < NO; ++m)
+  for (int n = 0; n < NJ; ++n) acc[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int n = 0; n < NJ; ++n) acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int h = 0; h < NH; ++h) acc4[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   // per lane and DMA instruction i: chunk e -> x chunk (plane c, row rr: image row
   // hr + rr d) or dy chunk (plane o, band row jr: image row r + (k0 + jr) d), as the
   // byte offset in its clip tensor at row 0 and the band row; kind 0 = zero chunk
@@ -900,30 +964,43 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
       const int pp = pv ? p : 0;
       const int row = div_small(pp, W, invW), col = pp - row * W;
       const float* xp = cur + row * G.Wr + col + TD_PAD - d;
-      float av[NO], bv[NJ];
-#pragma unroll
-      for (int m = 0; m < NO; ++m) {
-        const int o = 16 * m + i16;
-        av[m] = (pv && o < C) ? dl[o * DS + pp] : 0.f;
-      }
+      // av0 lane (kk, i16) = dy(o = i16, pixel 4 s + kk); av1 the same for o = 16 + i16,
+      // read by lanes i16 < 4 (block 4 kk of the 4x4 MFMA)
+      const float av0 = pv ? dl[i16 * DS + pp] : 0.f;
+      const float av1 = (pv && i16 < 4 && 16 + i16 < C) ? dl[(16 + i16) * DS + pp] : 0.f;
+      float bv[4 * NH];
 #pragma unroll
       for (int n = 0; n < NJ; ++n) bv[n] = xp[joff[n]];
 #pragma unroll
-      for (int m = 0; m < NO; ++m)
+      for (int n = NJ; n < 4 * NH; ++n) bv[n] = 0.f;
 #pragma unroll
-        for (int n = 0; n < NJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+      for (int n = 0; n < NJ; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av0, bv[n], acc[n], 0, 0, 0);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        tr4_rows(bv[4 * h], bv[4 * h + 1], bv[4 * h + 2], bv[4 * h + 3]);  // lane l: x(j = 64 h + l, pixel 4 s + q)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc4[h] = mfma4_bc(av1, bv[4 * h + q], acc4[h], 4 * q);
+      }
     }
   }
   td_wait_vm0();
   float* pb = a.part + (size_t)blockIdx.x * C * K9;
   constexpr int NJP = NJ * 16;
 #pragma unroll
-  for (int m = 0; m < NO; ++m) {
+  for (int m = 0; m < 2; ++m) {
     __syncthreads();
+    if (m == 0) {
 #pragma unroll
-    for (int n = 0; n < NJ; ++n)
+      for (int n = 0; n < NJ; ++n)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) tdl[(wave * 16 + 4 * kk + i) * NJP + 16 * n + i16] = acc[m][n][i];
+        for (int i = 0; i < 4; ++i) tdl[(wave * 16 + 4 * kk + i) * NJP + 16 * n + i16] = acc[n][i];
+    } else {
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (64 * h + lane < NJP) tdl[(wave * 16 + i) * NJP + 64 * h + lane] = acc4[h][i];
+    }
     __syncthreads();
     for (int idx = tid; idx < 16 * K9; idx += 512) {
       const int i = idx / K9, j = idx - i * K9, o = 16 * m + i;
