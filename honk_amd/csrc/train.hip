@@ -402,15 +402,19 @@ __host__ __device__ inline TdGeo td_geo(int C, int W, int TH) {
   return g;
 }
 
-// The 16x16x4 MFMA puts output channels 0..15 on one tile; channels 16..C-1 (C <= 20)
-// run on v_mfma_f32_4x4x1_16b_f32 (16 blocks of 4 x 4): the weight of one k for 4
-// channels is broadcast to all 16 blocks (CBSZ = 4, ABID = the source block), each
-// block takes 4 of the 64 pixels of a super tile.  19 channels: 16 + 4 rows instead
-// of 2 x 16 (0.95 instead of 0.59 of the MFMA rows do work).  The 4x4 operand (one
-// k, 64 pixels per register) is the 16x16x4 operands (4 k x 16 pixels, four
-// registers for 64 pixels) transposed by 16-lane rows: two permlane32 and two
-// permlane16 swaps.  Both accumulate k = 9 c + t in ascending order, one fmaf per k
-// (the VALU kernel's chain): bit-identical to it.
+// f(std::integral_constant<int, 0>{}) .. f(std::integral_constant<int, N - 1>{}): a
+// compile-time index (an MFMA's ABID must be a constant)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// 16-lane row transpose and the broadcast 4x4x1 MFMA (wgrad3x3d_kernel's output
+// channels 16..C-1; conv3x3d_kernel's every channel).
 __device__ __forceinline__ void tr4_rows(float& x0, float& x1, float& x2, float& x3) {
   // on exit 16-lane row g of x_q holds row q of x_g (on entry)
   const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x0), __float_as_uint(x2), false, false);
@@ -436,35 +440,36 @@ __device__ __forceinline__ f32x4_t mfma4_bc(float a, float b, f32x4_t c, int abi
   }
 }
 
+// conv3x3d_kernel: every output channel on v_mfma_f32_4x4x1_16b_f32 (16 blocks of
+// 4 x 4).  A wave takes a super tile of 64 pixels, lane l = pixel l; per k = 9 c + t
+// one LDS read (x at tap t of plane c, a uniform offset) feeds ceil(C/4) MFMAs, the
+// weights of 4 channels for k broadcast from the block that holds them (CBSZ = 4,
+// ABID = k mod 16; lane 4 b + r of wt[g][j] = w[4 g + r][16 j + b]).  19 channels use
+// 20 MFMA rows (a 16x16x4 tile pair would use 32), and the operands need neither a
+// transpose nor a second read.  Each output accumulates k in ascending order, one
+// fmaf per k: bit-identical to the VALU kernel's chain.
 template <int C>
 __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
-  static_assert(C > 16 && C <= 20, "conv3x3d_kernel: 16 < C <= 20");
-  constexpr int K = 9 * C, KS = (K + 3) / 4, KT = (K + 15) / 16;
+  static_assert(C <= 20, "conv3x3d_kernel: C <= 20");
+  constexpr int K = 9 * C, KT = (K + 15) / 16, NG = (C + 3) / 4, PF = 8;  // PF: reads in flight
   __shared__ __attribute__((aligned(16))) float tdl[2 * TD_BUF / 4];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i16 = lane & 15, kk = lane >> 4;
   const int d = a.g.d, W = a.W, H = a.H;
   const TdGeo G = td_geo(C, W, a.g.TH);
-  auto wv = [&](int o, int k) -> float {  // the layer weight of output o, k = 9 c + t
-    if (o >= C || k >= K) return 0.f;
-    const int c = k / 9, t = k - 9 * c;
-    return a.flip ? a.w[(c * C + o) * 9 + 8 - t] : a.w[(o * C + c) * 9 + t];
-  };
-  float wr[KS];  // 16x16x4 A operand: lane (kk, i16) = w[i16][4 s + kk]
-  float wt[KT];  // 4x4 A operand: lane 4 b + r = w[16 + r][16 j + b]
-  unsigned koff[(KS + 1) / 2];
+  float wt[NG][KT];
 #pragma unroll
-  for (int s = 0; s < (KS + 1) / 2; ++s) koff[s] = 0;
+  for (int g = 0; g < NG; ++g)
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int k = 4 * s + kk, c = k / 9, t = k - 9 * c;
-    wr[s] = wv(i16, k);
-    const unsigned off = k < K ? (unsigned)(c * G.PS + (t / 3) * G.Wr + (t % 3) * d) : 0u;
-    koff[s >> 1] |= off << (16 * (s & 1));
-  }
-#pragma unroll
-  for (int j = 0; j < KT; ++j) wt[j] = wv(16 + (lane & 3), 16 * j + (lane >> 2));
+    for (int j = 0; j < KT; ++j) {
+      const int o = 4 * g + (lane & 3), k = 16 * j + (lane >> 2);
+      float v = 0.f;
+      if (o < C && k < K) {
+        const int c = k / 9, t = k - 9 * c;
+        v = a.flip ? a.w[(c * C + o) * 9 + 8 - t] : a.w[(o * C + c) * 9 + t];
+      }
+      wt[g][j] = v;
+    }
   // per lane and DMA instruction i: chunk e = (wave TD_ITER + i) 64 + lane of the
   // buffer -> (plane c, row rr, 16-B column cc); tile-invariant byte offset of the
   // chunk in its clip (row 0), or -1 for a zero chunk
@@ -496,6 +501,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
           16, voff, 0, 0, 0);
     }
   };
+  // uniform LDS offset of tap t of plane c
+  const int PS = G.PS, Wr = G.Wr;
+  auto kof = [&](int k) {
+    const int c = k / 9, t = k - 9 * c;
+    return c * PS + (t / 3) * Wr + (t % 3) * d;
+  };
   float* buf0 = tdl;
   float* buf1 = tdl + TD_BUF / 4;
   if ((int)blockIdx.x < ntile) issue(blockIdx.x, buf0);
@@ -512,51 +523,36 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
     const int npx = th * W, nst = (npx + 63) >> 6;
     float* yb = a.y + (size_t)b * clip;
     for (int m = wave; m < nst; m += 8) {  // super tile m: pixels 64 m .. 64 m + 63 of the band
-      int xo[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int p = 64 * m + 16 * g + i16;
-        const int pp = p < npx ? p : 0, j = pp / W, col = pp - j * W;
-        xo[g] = j * G.Wr + col + TD_PAD - d;
-      }
-      f32x4_t acc[4], acc4 = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      auto kof = [&](int s) { return (int)((koff[s >> 1] >> (16 * (s & 1))) & 0xffffu); };
-      float xv[4];  // the operands of k-step s; those of s + 1 are read before s's MFMAs
-#pragma unroll
-      for (int g = 0; g < 4; ++g) xv[g] = cur[xo[g] + kof(0)];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        float xn[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) xn[g] = s + 1 < KS ? cur[xo[g] + kof(s + 1)] : 0.f;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s], xv[g], acc[g], 0, 0, 0);
-        tr4_rows(xv[0], xv[1], xv[2], xv[3]);  // xv[q] lane l = x(k = 4 s + q, pixel 64 m + l)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (4 * s + q < K) acc4 = mfma4_bc(wt[(4 * s + q) >> 4], xv[q], acc4, 4 * s + q);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) xv[g] = xn[g];
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int p = 64 * m + 16 * g + i16;
-        if (p < npx) {
-          const int j = p / W, col = p - j * W;
-          const size_t pix = (size_t)(r + (k0 + j) * d) * W + col;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) yb[(size_t)(4 * kk + i) * H * W + pix] = acc[g][i];
-        }
-      }
       const int p = 64 * m + lane;
-      if (p < npx) {
-        const int j = p / W, col = p - j * W;
+      const bool pv = p < npx;
+      const int j = pv ? p / W : 0, col = pv ? p - j * W : 0;
+      const float* xp = cur + j * Wr + col + TD_PAD - d;
+      f32x4_t acc[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      float xr[PF];  // ring of operands read PF k ahead (PF divides 16: slots are compile-time)
+#pragma unroll
+      for (int k = 0; k < PF; ++k) xr[k] = xp[kof(k)];
+#pragma unroll
+      for (int jj = 0; jj < KT; ++jj)
+        static_for<16>([&](auto bc) {
+          constexpr int B = decltype(bc)::value;
+          const int k = 16 * jj + B;
+          if (k < K) {
+            const float xv = xr[B % PF];
+            xr[B % PF] = xp[kof(k + PF < K ? k + PF : K - 1)];
+#pragma unroll
+            for (int g = 0; g < NG; ++g) acc[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(wt[g][jj], xv, acc[g], 4, B, 0);
+            __builtin_amdgcn_sched_barrier(0);  // keeps each read PF k ahead of its use
+          }
+        });
+      if (pv) {
         const size_t pix = (size_t)(r + (k0 + j) * d) * W + col;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (16 + i < C) yb[(size_t)(16 + i) * H * W + pix] = acc4[i];
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (4 * g + i < C) yb[(size_t)(4 * g + i) * H * W + pix] = acc[g][i];
       }
     }
   }
@@ -958,29 +954,46 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
     band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
     const int npx = th * W, nks = (npx + 3) >> 2;
     const float* dl = cur + XF;
-    for (int s = wave; s < nks; s += 8) {
+    // operands of k-step s + 8 (this wave's next) are read before step s's MFMAs; the
+    // 4x4 MFMAs interleave with the 16x16x4 ones (acc4[h] in q order)
+    auto ld = [&](int s, float& a0, float& a1, float* bv) {
       const int p = 4 * s + kk;
       const bool pv = p < npx;
       const int pp = pv ? p : 0;
       const int row = div_small(pp, W, invW), col = pp - row * W;
       const float* xp = cur + row * G.Wr + col + TD_PAD - d;
-      // av0 lane (kk, i16) = dy(o = i16, pixel 4 s + kk); av1 the same for o = 16 + i16,
+      // a0 lane (kk, i16) = dy(o = i16, pixel 4 s + kk); a1 the same for o = 16 + i16,
       // read by lanes i16 < 4 (block 4 kk of the 4x4 MFMA)
-      const float av0 = pv ? dl[i16 * DS + pp] : 0.f;
-      const float av1 = (pv && i16 < 4 && 16 + i16 < C) ? dl[(16 + i16) * DS + pp] : 0.f;
-      float bv[4 * NH];
+      a0 = pv ? dl[i16 * DS + pp] : 0.f;
+      a1 = (pv && i16 < 4 && 16 + i16 < C) ? dl[(16 + i16) * DS + pp] : 0.f;
 #pragma unroll
       for (int n = 0; n < NJ; ++n) bv[n] = xp[joff[n]];
 #pragma unroll
       for (int n = NJ; n < 4 * NH; ++n) bv[n] = 0.f;
+    };
+    auto step = [&](float a0, float a1, const float* bv) {
+      float bt[4 * NH];
 #pragma unroll
-      for (int n = 0; n < NJ; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av0, bv[n], acc[n], 0, 0, 0);
+      for (int n = 0; n < 4 * NH; ++n) bt[n] = bv[n];
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        tr4_rows(bv[4 * h], bv[4 * h + 1], bv[4 * h + 2], bv[4 * h + 3]);  // lane l: x(j = 64 h + l, pixel 4 s + q)
+      for (int h = 0; h < NH; ++h)
+        tr4_rows(bt[4 * h], bt[4 * h + 1], bt[4 * h + 2], bt[4 * h + 3]);  // lane l: x(j = 64 h + l, pixel 4 s + q)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc4[h] = mfma4_bc(av1, bv[4 * h + q], acc4[h], 4 * q);
+      for (int n = 0; n < 4 * NH; ++n) {
+        if (n < NJ) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv[n], acc[n], 0, 0, 0);
+        const int h = n % NH, q = n / NH;
+        acc4[h] = mfma4_bc(a1, bt[4 * h + q], acc4[h], 4 * q);
       }
+    };
+    // two operand sets in turn (no register moves between steps)
+    float e0 = 0.f, e1 = 0.f, ev[4 * NH], o0 = 0.f, o1 = 0.f, ov[4 * NH];
+    if (wave < nks) ld(wave, e0, e1, ev);
+    for (int s = wave; s < nks; s += 16) {
+      ld(s + 8 < nks ? s + 8 : s, o0, o1, ov);
+      step(e0, e1, ev);
+      if (s + 8 >= nks) break;
+      ld(s + 16 < nks ? s + 16 : s, e0, e1, ev);
+      step(o0, o1, ov);
     }
   }
   td_wait_vm0();
