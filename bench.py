@@ -462,6 +462,7 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
     over RCCL when world > 1, fused SGD).  Roofline: algorithmic training FLOP per
     step / step time vs the fp32 peak (the native training convs are fp32)."""
     from honk_amd import model as hm
+    from honk_amd.head_train import CrossEntropyLoss
     from honk_amd.optim import FlatParams, FlatSGD
     hd = ctx.hd
     B = B or 4096
@@ -471,7 +472,7 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
     hd.broadcast_module(model)
     flat = FlatParams(model)
     opt = FlatSGD(flat, lr=0.1, momentum=0.9, weight_decay=1e-5)
-    crit = torch.nn.CrossEntropyLoss()
+    crit = CrossEntropyLoss()
     g = torch.Generator(device=ctx.dev).manual_seed(99 + ctx.rank)
     x = torch.randn(B, 101, 40, device=ctx.dev, generator=g)
     y = torch.randint(0, cfg["n_labels"], (B,), device=ctx.dev, generator=g)
@@ -514,8 +515,8 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
                      "flop_def": "2 x (forward + input-grad + weight-grad MACs), conv0 has no input grad"},
         "note": "native kernels: the stem (conv0 + relu + avg-pool, conv0 weight grad), the block convs' "
                 "forward / input grad / weight grad on fp32 MFMA, each block's relu + residual + train-mode "
-                "BatchNorm fwd/bwd fused, fused SGD over the flat all-reduced bucket; the mean, Linear and the "
-                "loss run on PyTorch autograd on the device"}
+                "BatchNorm fwd/bwd fused, the spatial mean, the Linear and the cross-entropy loss "
+                "(honk_amd/head_train.py), fused SGD over the flat all-reduced bucket"}
 
 
 def rank_main(args):

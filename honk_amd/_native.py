@@ -92,6 +92,15 @@ _PROTOS = {
                                 + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "honk_mfcc_f32": (ctypes.c_int, [c_f32p, ctypes.c_int64, ctypes.c_int32, c_f32p, ctypes.c_int32, ctypes.c_int32,
                                      c_f32p, ctypes.c_int32, c_f32p, ctypes.c_int32, c_f32p, ctypes.c_void_p]),
+    "honk_spatial_mean_f32": (ctypes.c_int, [c_f32p, c_f32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]),
+    "honk_spatial_mean_bwd_f32": (ctypes.c_int, [c_f32p, c_f32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]),
+    "honk_cross_entropy_f32": (ctypes.c_int, [c_f32p, ctypes.c_void_p, c_f32p, ctypes.c_int64, ctypes.c_int32,
+                                              ctypes.c_void_p]),
+    "honk_cross_entropy_bwd_f32": (ctypes.c_int, [c_f32p, ctypes.c_void_p, c_f32p, c_f32p, ctypes.c_int64,
+                                                  ctypes.c_int32, ctypes.c_void_p]),
+    "honk_augment_f32": (ctypes.c_int, [c_f32p, c_f32p] + [ctypes.c_void_p] * 2 + [c_f32p, ctypes.c_void_p, c_f32p,
+                                                                                    ctypes.c_int64, ctypes.c_int32,
+                                                                                    ctypes.c_int64, ctypes.c_void_p]),
     "honk_last_error": (ctypes.c_char_p, []),
     "honk_version": (ctypes.c_char_p, []),
     "honk_timing_enable": (ctypes.c_int, [ctypes.c_int32]),

@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhonk_hip.so")
-SOURCES = ["runtime.cpp", "res.hip", "cnn.hip", "train.hip", "mfcc.hip"]
+SOURCES = ["runtime.cpp", "res.hip", "cnn.hip", "train.hip", "mfcc.hip", "head.hip", "augment.hip"]
 ARCH = os.environ.get("HONK_OFFLOAD_ARCH", "gfx950")
 
 

@@ -21,8 +21,9 @@ Forward dispatch:
   stem (conv0 + relu + avg-pool), the block convs (every dilation) and each
   block's relu / residual / train-mode BatchNorm run on the native training
   kernels (``honk_amd/conv3x3.py``), and so do SpeechModel's relu(conv) layers
-  and max-pools (``honk_amd/cnn_train.py``); dropout, the mean, the Linear
-  layers and the loss stay PyTorch.
+  and max-pools (``honk_amd/cnn_train.py``) and both families' head: the spatial
+  mean and the Linear layers (``honk_amd/head_train.py``; the loss is
+  ``head_train.CrossEntropyLoss``); dropout stays PyTorch's own op (its RNG).
 """
 from __future__ import annotations
 
@@ -34,6 +35,7 @@ import torch.nn.functional as F
 
 from . import _native
 from . import cnn_train as _cnn_train
+from . import head_train as _head
 from . import conv3x3 as _conv3x3
 
 
@@ -161,7 +163,7 @@ class SpeechResModel(SerializableModule):
     # honk_res_stem_*, the block convs (conv1..convN) on honk_conv3x3_f32 /
     # honk_conv3x3_wgrad_f32 where they cover the shape (any dilation, 19 or 45 maps)
     # and each block's relu / residual / train-mode BatchNorm on honk_res_tail_*
-    # (honk_amd/conv3x3.py); the mean, Linear and the loss stay PyTorch autograd
+    # (honk_amd/conv3x3.py), the mean and the Linear on honk_amd/head_train.py
     def _torch_forward(self, x, native_convs=False):
         x_in, x = x, x.unsqueeze(1)
         for i in range(self.n_layers + 1):
@@ -209,6 +211,8 @@ class SpeechResModel(SerializableModule):
                     if native_convs and bn.training:
                         _conv3x3.warn_fallback(self, "train-mode BatchNorm")
                     x = bn(x)
+        if native_convs and _head.supported(x):
+            return _head.linear(_head.spatial_mean(x), self.output)
         x = x.view(x.size(0), x.size(1), -1)  # shape: (batch, feats, o3)
         x = torch.mean(x, 2)
         return self.output(x)
@@ -367,8 +371,8 @@ class SpeechModel(SerializableModule):
 
     # -- reference forward (CPU tensors / training mode): model.py:186-205 --
     # native: training on a ROCm tensor runs relu(conv) and the max-pools on the
-    # native training kernels (honk_amd/cnn_train.py); dropout, the Linear layers and
-    # the loss stay PyTorch autograd on the device
+    # native training kernels (honk_amd/cnn_train.py) and the Linear layers (dnn1's
+    # ReLU fused) on honk_amd/head_train.py; dropout stays PyTorch's op (its RNG stream)
     def _conv_relu(self, conv, x, native):
         if native and _cnn_train.conv_supported(x, conv):
             return _cnn_train.conv_relu(x, conv)
@@ -392,17 +396,21 @@ class SpeechModel(SerializableModule):
             x = self.dropout(x)
             x = self._pool(self.pool2, x, native)
         x = x.view(x.size(0), -1)  # shape: (batch, o3)
+        lin = native and _head.supported(x)
         if hasattr(self, "lin"):
-            x = self.lin(x)
+            x = _head.linear(x, self.lin) if lin else self.lin(x)
         if hasattr(self, "dnn1"):
-            x = self.dnn1(x)
-            if not self.tf_variant:
-                x = F.relu(x)
+            if lin and not self.tf_variant:
+                x = _head.linear_relu(x, self.dnn1)
+            else:
+                x = _head.linear(x, self.dnn1) if lin else self.dnn1(x)
+                if not self.tf_variant:
+                    x = F.relu(x)
             x = self.dropout(x)
         if hasattr(self, "dnn2"):
-            x = self.dnn2(x)
+            x = _head.linear(x, self.dnn2) if lin else self.dnn2(x)
             x = self.dropout(x)
-        return self.output(x)
+        return _head.linear(x, self.output) if lin else self.output(x)
 
     def _native_tensors(self):
         def wb(name):

@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.utils.data as data
 
 from . import distributed as hd
+from . import head_train
 from . import model as mod
 from .optim import FlatParams, FlatSGD
 
@@ -159,7 +160,7 @@ def train(config, datasets=None):
     schedule_steps = config["schedule"]  # the caller's list, extended in place (utils/train.py:100-101)
     schedule_steps.append(np.inf)
     sched_idx = 0
-    criterion = nn.CrossEntropyLoss()
+    criterion = head_train.CrossEntropyLoss()  # nn.CrossEntropyLoss(); native on ROCm tensors
     max_acc = 0
     best_model = None
 

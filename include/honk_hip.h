@@ -260,6 +260,38 @@ int honk_res_stem_wgrad_f32(const float* x, const float* w0, const float* gy, fl
                             int32_t h, int32_t w_, int32_t ph, int32_t pw, void* workspace, size_t workspace_bytes,
                             void* stream);
 
+/*
+ * The training step's head (utils/train.py:129-131 with model.py:119-121): the
+ * spatial mean z[r] = sum_i x[r][i] / hw over rows r = (b, c) (x.view(B, C, -1) then
+ * torch.mean(x, 2)) and its backward gx[r][i] = gz[r] / hw; nn.CrossEntropyLoss()
+ * (mean reduction): *loss = mean_b (logsumexp(z_b) - z_b[labels_b]) (a label outside
+ * [0, n) gives NaN), and dlogits = (softmax(z_b) - onehot(labels_b)) * (*grad_loss) / batch
+ * (grad_loss: the device scalar upstream gradient).  Fixed-order reductions.
+ */
+int honk_spatial_mean_f32(const float* x, float* z, int64_t rows, int32_t hw, void* stream);
+int honk_spatial_mean_bwd_f32(const float* gz, float* gx, int64_t rows, int32_t hw, void* stream);
+int honk_cross_entropy_f32(const float* logits, const int64_t* labels, float* loss, int64_t batch, int32_t n,
+                           void* stream);
+int honk_cross_entropy_bwd_f32(const float* logits, const int64_t* labels, const float* grad_loss, float* dlogits,
+                               int64_t batch, int32_t n, void* stream);
+
+/*
+ * Training-set audio augmentation (SpeechDataset.load_audio, utils/model.py:282-306,
+ * with _timeshift_audio :264-270), the per-clip transform on a batch of PCM
+ * audio/out [batch][len] (the clips right-padded to len); the random draws are the
+ * caller's (honk_amd/augment.py draws them on the reference's `random` stream):
+ *   v[i] = (flags & HONK_AUG_SILENCE) ? 0 : (0 <= i + shift < len ? audio[i + shift] : 0)
+ *   out[i] = (flags & HONK_AUG_NOISE) ? clip(amp * noise[noise_off + i] + v[i], -1, 1) : v[i]
+ * in float32 (product rounded, then the sum; NaN kept).  shift/noise_off/amp/flags are
+ * [batch] device arrays; noise is the concatenated background-noise bank
+ * [noise_len] (NULL iff noise_len == 0; reads outside it are 0).  batch <= 65535.
+ */
+#define HONK_AUG_SILENCE 1
+#define HONK_AUG_NOISE 2
+int honk_augment_f32(const float* audio, const float* noise, const int32_t* shift, const int64_t* noise_off,
+                     const float* amp, const int32_t* flags, float* out, int64_t batch, int32_t len,
+                     int64_t noise_len, void* stream);
+
 /* ---- diagnostics --------------------------------------------------------------- */
 const char* honk_last_error(void);
 const char* honk_version(void);

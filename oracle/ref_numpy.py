@@ -350,3 +350,31 @@ def cnn_flops_per_clip(cfg):
 
 def flops_per_clip(cfg):
     return res_flops_per_clip(cfg) if "n_layers" in cfg else cnn_flops_per_clip(cfg)
+
+
+# --------------------------------------------------------------------------- #
+# training-set augmentation: SpeechDataset.load_audio's transform given its draws
+# (model.py:282-306, _timeshift_audio :264-270), the same NumPy operations
+# --------------------------------------------------------------------------- #
+def timeshift(data, shift):
+    """_timeshift_audio with the drawn shift (model.py:265-270)."""
+    a = -min(0, shift)
+    b = max(0, shift)
+    data = np.pad(data, (a, b), "constant")
+    return data[:len(data) - a] if a else data[b:]
+
+
+def augment_clip(data, bg_slice, shift, amp, silence, mix, input_length, train=True):
+    """load_audio after its draws (model.py:290-306): data the clip (float32; ignored
+    for silence), bg_slice the drawn noise slice (float32, or None: np.zeros(input_length)
+    as the reference uses without noise files), amp the drawn Python float a."""
+    if bg_slice is None:
+        bg_slice = np.zeros(input_length)
+    if silence:
+        data = np.zeros(input_length, dtype=np.float32)
+    data = np.pad(data, (0, max(0, input_length - len(data))), "constant")
+    if train:
+        data = timeshift(data, shift)
+    if mix:
+        data = np.clip(amp * bg_slice + data, -1, 1)
+    return data

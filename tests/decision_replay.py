@@ -21,8 +21,8 @@ On the same piece of the piecewise-smooth function the two must agree to fp32
 rounding times the step's smooth conditioning (~7 for res26-narrow).
 
 Sites: SpeechResModel -- the stem ReLU (the native stem's mask observed by an unpooled
-run of the same kernel) and every block's ReLU; SpeechModel -- relu(conv1), relu(conv2), the dnn1 ReLU and
-the max-pools.  Reference lines: model.py:104-121 (res), :186-205 (cnn).
+run of the same kernel) and every block's ReLU; SpeechModel -- relu(conv1), relu(conv2), the dnn1 ReLU
+(fused into the native Linear: ``head_train.linear_relu``) and the max-pools.  Reference lines: model.py:104-121 (res), :186-205 (cnn).
 """
 from __future__ import annotations
 
@@ -34,6 +34,7 @@ import torch.nn.functional as F
 
 from honk_amd import cnn_train as _ct
 from honk_amd import conv3x3 as _c3
+from honk_amd import head_train as _ht
 from honk_amd import model as hm
 
 
@@ -59,6 +60,7 @@ def record(dec: Decisions):
     orig_conv3 = _c3.conv3x3
     orig_stem = _c3.stem
     orig_crelu = _ct.conv_relu
+    orig_lrelu = _ht.linear_relu
     orig_pool = hm.SpeechModel._pool
 
     def relu(x, inplace=False):
@@ -83,6 +85,11 @@ def record(dec: Decisions):
         dec.relu.append((y > 0).detach().cpu())
         return y
 
+    def lrelu(x, lin):
+        y = orig_lrelu(x, lin)
+        dec.relu.append((y > 0).detach().cpu())
+        return y
+
     def pool(self, p, x, native):
         k = _pool_k(p)
         if k == (1, 1):
@@ -95,6 +102,7 @@ def record(dec: Decisions):
     _c3.conv3x3 = conv3
     _c3.stem = stem
     _ct.conv_relu = crelu
+    _ht.linear_relu = lrelu
     hm.SpeechModel._pool = pool
     try:
         yield dec
@@ -103,6 +111,7 @@ def record(dec: Decisions):
         _c3.conv3x3 = orig_conv3
         _c3.stem = orig_stem
         _ct.conv_relu = orig_crelu
+        _ht.linear_relu = orig_lrelu
         hm.SpeechModel._pool = orig_pool
 
 
