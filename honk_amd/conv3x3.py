@@ -94,25 +94,67 @@ def _wgrad(x, dy, d=1):
     return dw
 
 
+STATS_USED = {"fwd": 0, "bwd": 0}   # tails that took the conv epilogue's statistics (tests)
+
+
+def _stats_buf(B, C, H, W, d, device):
+    """The statistics buffer of the conv epilogue for this shape, or None (no epilogue)."""
+    n = int(_native.load().honk_conv3x3_stats_bytes(B, C, H, W, d))
+    return torch.empty(n, dtype=torch.uint8, device=device) if n else None
+
+
+def _conv_stats(x, w, flip, d, mode, aux, buf):
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    y = torch.empty_like(x)
+    _native.check(_native.load().honk_conv3x3_stats_f32(
+        x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W, d, 1 if flip else 0, mode,
+        aux.data_ptr() if aux is not None else None, buf.data_ptr(), buf.numel(), _native.stream_handle(x.device)),
+        "honk_conv3x3_stats_f32")
+    return y
+
+
 class _Conv3x3(torch.autograd.Function):
+    """h = conv(x, w).  Statistics boxes (dicts shared with honk_amd's res tails, see
+    res_tail): box_out -> this conv's epilogue also sums the next tail's forward
+    statistics (of relu(h) [+ old]) into box_out["fwd"]; box_in (the box of the tail
+    whose output x is) -> the input-gradient conv sums that tail's backward statistics
+    (of dx and dx * x) into box_in["bwd"] = (buffer, dx)."""
+
     @staticmethod
-    def forward(ctx, x, w, d):
+    def forward(ctx, x, w, d, old, box_out, box_in):
         w = w.contiguous()
         ctx.save_for_backward(x, w)
         ctx.dil = d
+        ctx.box_in = box_in
+        if box_out is not None:
+            B, C, H, W = x.shape
+            buf = _stats_buf(B, C, H, W, d, x.device)
+            if buf is not None:
+                box_out["fwd"] = (buf, d)   # partials laid out by this conv's grid (its dilation)
+                return _conv_stats(x, w, False, d, 1, old.contiguous() if old is not None else None, buf)
         return _conv(x, w, flip=False, d=d)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dy = dy.contiguous()
-        dx = _conv(dy, w, flip=True, d=ctx.dil) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            box = ctx.box_in
+            B, C, H, W = x.shape
+            buf = _stats_buf(B, C, H, W, ctx.dil, x.device) if box is not None else None
+            if buf is not None:
+                dx = _conv_stats(dy, w, True, ctx.dil, 2, x.contiguous(), buf)
+                box["bwd"] = (buf, dx, dx._version, ctx.dil)
+            else:
+                dx = _conv(dy, w, flip=True, d=ctx.dil)
         dw = _wgrad(x, dy, d=ctx.dil) if ctx.needs_input_grad[1] else None
-        return dx, dw, None
+        return dx, dw, None, None, None, None
 
 
-def conv3x3(x, w, d=1):
-    return _Conv3x3.apply(x, w, int(d))
+def conv3x3(x, w, d=1, old=None, box_out=None, box_in=None):
+    return _Conv3x3.apply(x, w, int(d), old, box_out, box_in)
 
 
 # -- train-mode BatchNorm2d(affine=False) (model.py:100, 117-118 in training) -------
@@ -155,10 +197,12 @@ class _BatchNormTrain(torch.autograd.Function):
 
 class _ResTail(torch.autograd.Function):
     """s = relu(h) [+ old]; y = BatchNorm_train(s) on honk_res_tail_fwd/bwd_f32
-    (model.py:111-118): returns y, or (y, s) when s feeds the next residual."""
+    (model.py:111-118): returns y, or (y, s) when s feeds the next residual.  With a
+    statistics box (conv3x3's box_out for h, box_in of the conv that reads y) the
+    statistics come from those convs' epilogues (honk_res_tail_*_part_f32)."""
 
     @staticmethod
-    def forward(ctx, h, old, running_mean, running_var, momentum, eps, keep_s):
+    def forward(ctx, h, old, running_mean, running_var, momentum, eps, keep_s, box):
         h = h.contiguous()
         old = old.contiguous() if old is not None else None
         B, C, H, W = h.shape
@@ -166,15 +210,23 @@ class _ResTail(torch.autograd.Function):
         s = torch.empty_like(h) if keep_s else None
         mean = torch.empty(C, dtype=torch.float32, device=h.device)
         invstd = torch.empty_like(mean)
-        ws, nb = _bn_ws(B, C, H * W, h.device)
         ptr = (lambda t: t.data_ptr() if t is not None else None)
-        _native.check(_native.load().honk_res_tail_fwd_f32(h.data_ptr(), ptr(old), ptr(s), y.data_ptr(),
-                                                           mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
-                                                           ptr(running_var), B, C, H * W, momentum, eps,
-                                                           ws.data_ptr(), nb, _native.stream_handle(h.device)),
-                      "honk_res_tail_fwd_f32")
+        st = _native.stream_handle(h.device)
+        if box is not None and "fwd" in box:
+            STATS_USED["fwd"] += 1
+            buf, d = box.pop("fwd")
+            _native.check(_native.load().honk_res_tail_fwd_part_f32(
+                h.data_ptr(), ptr(old), ptr(s), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
+                ptr(running_var), buf.data_ptr(), B, C, H, W, d, momentum, eps, st), "honk_res_tail_fwd_part_f32")
+        else:
+            ws, nb = _bn_ws(B, C, H * W, h.device)
+            _native.check(_native.load().honk_res_tail_fwd_f32(h.data_ptr(), ptr(old), ptr(s), y.data_ptr(),
+                                                               mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
+                                                               ptr(running_var), B, C, H * W, momentum, eps,
+                                                               ws.data_ptr(), nb, st), "honk_res_tail_fwd_f32")
         ctx.save_for_backward(h, y, invstd)
         ctx.has_old = old is not None
+        ctx.box = box
         if keep_s:
             return y, s
         return y
@@ -185,25 +237,37 @@ class _ResTail(torch.autograd.Function):
         B, C, H, W = y.shape
         if gy is None:
             gy = torch.zeros_like(y)
-        gy = gy.contiguous()
         gs = gs.contiguous() if gs is not None else None
         gh = torch.empty_like(y)
         gold = torch.empty_like(y) if ctx.has_old and ctx.needs_input_grad[1] else None
-        ws, nb = _bn_ws(B, C, H * W, y.device)
         ptr = (lambda t: t.data_ptr() if t is not None else None)
-        _native.check(_native.load().honk_res_tail_bwd_f32(gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(),
-                                                           h.data_ptr(), gh.data_ptr(), ptr(gold), B, C, H * W,
-                                                           ws.data_ptr(), nb, _native.stream_handle(y.device)),
-                      "honk_res_tail_bwd_f32")
-        return gh, gold, None, None, None, None, None
+        st = _native.stream_handle(y.device)
+        pre = ctx.box.pop("bwd", None) if ctx.box is not None else None
+        if pre is not None and pre[1] is gy and gy._version == pre[2]:
+            # the statistics of exactly this gradient, summed by the conv that produced it
+            STATS_USED["bwd"] += 1
+            _native.check(_native.load().honk_res_tail_bwd_part_f32(
+                gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(), h.data_ptr(), gh.data_ptr(), ptr(gold),
+                pre[0].data_ptr(), B, C, H, W, pre[3], st), "honk_res_tail_bwd_part_f32")
+        else:
+            gy = gy.contiguous()
+            ws, nb = _bn_ws(B, C, H * W, y.device)
+            _native.check(_native.load().honk_res_tail_bwd_f32(gy.data_ptr(), ptr(gs), y.data_ptr(),
+                                                               invstd.data_ptr(), h.data_ptr(), gh.data_ptr(),
+                                                               ptr(gold), B, C, H * W, ws.data_ptr(), nb, st),
+                          "honk_res_tail_bwd_f32")
+        return gh, gold, None, None, None, None, None, None
 
 
-def res_tail(h, old, bn, keep_s=False):
+def res_tail(h, old, bn, keep_s=False, box=None):
     """The res block tail in training (model.py:111-118): x = relu(h); x = x + old
     (old not None); old_x = x; x = bn(x) -- one native kernel chain, bit-identical
-    to the unfused PyTorch ops.  Returns bn's output, or (output, old_x) if keep_s."""
+    to the unfused PyTorch ops (with a statistics box, box["fwd"] from the conv that
+    made h: the same ops with the statistics from that conv's epilogue).  Returns
+    bn's output, or (output, old_x) if keep_s."""
     bn.num_batches_tracked.add_(1)
-    out = _ResTail.apply(h, old, bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps), bool(keep_s))
+    out = _ResTail.apply(h, old, bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps), bool(keep_s),
+                         box)
     torch.autograd.graph.increment_version(bn.running_mean)
     torch.autograd.graph.increment_version(bn.running_var)
     return out

@@ -120,6 +120,9 @@ struct Conv3Args {
   float* y;        // [B][C][H][W]
   int B, H, W, flip;
   ClassBands g;
+  // conv3x3d_kernel's BatchNorm statistics epilogue (MODE 1 / 2), else unused:
+  const float* aux;  // MODE 1: the residual old (may be null); MODE 2: the BN output y
+  double* part;      // [C][gridDim.x][2] per-workgroup partial sums
 };
 
 typedef float tf2 __attribute__((ext_vector_type(2)));
@@ -448,7 +451,14 @@ __device__ __forceinline__ f32x4_t mfma4_bc(float a, float b, f32x4_t c, int abi
 // 20 MFMA rows (a 16x16x4 tile pair would use 32), and the operands need neither a
 // transpose nor a second read.  Each output accumulates k in ascending order, one
 // fmaf per k: bit-identical to the VALU kernel's chain.
-template <int C>
+// MODE (the statistics epilogue; partial sums per workgroup, fixed-order reductions):
+//   0: none;
+//   1: the res tail's forward statistics of s = relu(h) [+ old] (tail_partial_kernel's
+//      sums: s and s*s) -- the pass over h and old that kernel makes is skipped;
+//   2: the BatchNorm backward statistics of gy = this (input-gradient) conv's output with
+//      the BN output y (bn_partial_kernel's sums: gy and gy*y).
+// Per lane fp32 sums over its pixels, then double across lanes and waves.
+template <int C, int MODE>
 __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
   static_assert(C <= 20, "conv3x3d_kernel: C <= 20");
   constexpr int K = 9 * C, KT = (K + 15) / 16, NG = (C + 3) / 4, PF = 8;  // PF: reads in flight
@@ -507,6 +517,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
     const int c = k / 9, t = k - 9 * c;
     return c * PS + (t / 3) * Wr + (t % 3) * d;
   };
+  float sa[MODE ? C : 1], sb[MODE ? C : 1];  // per-lane statistics (MODE 1 / 2)
+#pragma unroll
+  for (int o = 0; o < (MODE ? C : 1); ++o) sa[o] = sb[o] = 0.f;
   float* buf0 = tdl;
   float* buf1 = tdl + TD_BUF / 4;
   if ((int)blockIdx.x < ntile) issue(blockIdx.x, buf0);
@@ -530,6 +543,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
       f32x4_t acc[NG];
 #pragma unroll
       for (int g = 0; g < NG; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      // the statistics epilogue's operand (old / y at this lane's pixel), read before the
+      // MFMAs so its latency hides behind them
+      float av[MODE ? C : 1];
+      const size_t pix = (size_t)(r + (k0 + j) * d) * W + col;
+      if constexpr (MODE != 0) {
+        const float* ab = a.aux ? a.aux + (size_t)b * clip + pix : nullptr;
+#pragma unroll
+        for (int o = 0; o < C; ++o) av[o] = (ab && pv) ? ab[(size_t)o * H * W] : 0.f;
+      }
       float xr[PF];  // ring of operands read PF k ahead (PF divides 16: slots are compile-time)
 #pragma unroll
       for (int k = 0; k < PF; ++k) xr[k] = xp[kof(k)];
@@ -547,16 +569,56 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
           }
         });
       if (pv) {
-        const size_t pix = (size_t)(r + (k0 + j) * d) * W + col;
 #pragma unroll
         for (int g = 0; g < NG; ++g)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (4 * g + i < C) yb[(size_t)(4 * g + i) * H * W + pix] = acc[g][i];
+          for (int i = 0; i < 4; ++i) {
+            const int o = 4 * g + i;
+            if (o < C) {
+              const float v = acc[g][i];
+              yb[(size_t)o * H * W + pix] = v;
+              if constexpr (MODE == 1) {
+                float sv = v <= 0.f ? 0.f : v;  // relu_f: NaN passes, as torch.relu
+                if (a.aux) sv = sv + av[o];
+                sa[o] += sv;
+                sb[o] += sv * sv;
+              } else if constexpr (MODE == 2) {
+                sa[o] += v;
+                sb[o] += v * av[o];
+              }
+            }
+          }
       }
     }
   }
   td_wait_vm0();  // no DMA left in flight when the workgroup retires
+  if constexpr (MODE != 0) {
+    __shared__ double red[8][C][2];
+#pragma unroll
+    for (int o = 0; o < C; ++o) {
+      double u = sa[o], v = sb[o];
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        u += __shfl_xor(u, m);
+        v += __shfl_xor(v, m);
+      }
+      if (lane == 0) {
+        red[wave][o][0] = u;
+        red[wave][o][1] = v;
+      }
+    }
+    __syncthreads();
+    if (tid < C) {
+      double u = 0.0, v = 0.0;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) {
+        u += red[w8][tid][0];
+        v += red[w8][tid][1];
+      }
+      a.part[((size_t)tid * gridDim.x + blockIdx.x) * 2] = u;
+      a.part[((size_t)tid * gridDim.x + blockIdx.x) * 2 + 1] = v;
+    }
+  }
 }
 
 // class rows per conv3x3d_kernel tile (0: not applicable): the largest band whose
@@ -1134,17 +1196,40 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const float* __restrict
   }
 }
 
-// forward: mean, invstd per channel; running stats (momentum, unbiased variance)
-__global__ void bn_stats_kernel(const double* __restrict__ part, float* __restrict__ mean, float* __restrict__ invstd,
-                                float* __restrict__ rmean, float* __restrict__ rvar, int C, int S, double n,
-                                float momentum, float eps) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int s = 0; s < S; ++s) {
-    s1 += part[((size_t)c * S + s) * 2];
-    s2 += part[((size_t)c * S + s) * 2 + 1];
+// the S (sum a, sum ab) partials of channel c = blockIdx.x, summed by one workgroup:
+// thread t takes slices t, t + 256, .. in order, then a fixed LDS tree
+__device__ __forceinline__ void bn_combine(const double* __restrict__ part, int S, double& s1, double& s2) {
+  __shared__ double r1[256], r2[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int s = t; s < S; s += 256) {
+    a += part[((size_t)c * S + s) * 2];
+    b += part[((size_t)c * S + s) * 2 + 1];
   }
+  r1[t] = a;
+  r2[t] = b;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (t < w) {
+      r1[t] += r1[t + w];
+      r2[t] += r2[t + w];
+    }
+    __syncthreads();
+  }
+  s1 = r1[0];
+  s2 = r2[0];
+}
+
+// forward: mean, invstd per channel; running stats (momentum, unbiased variance).
+// One workgroup of 256 threads per channel.
+__global__ __launch_bounds__(256) void bn_stats_kernel(const double* __restrict__ part, float* __restrict__ mean,
+                                                       float* __restrict__ invstd, float* __restrict__ rmean,
+                                                       float* __restrict__ rvar, int C, int S, double n,
+                                                       float momentum, float eps) {
+  double s1, s2;
+  bn_combine(part, S, s1, s2);
+  const int c = blockIdx.x;
+  if (threadIdx.x != 0) return;
   const double m = s1 / n;
   double var = s2 / n - m * m;
   if (var < 0.0) var = 0.0;
@@ -1156,18 +1241,14 @@ __global__ void bn_stats_kernel(const double* __restrict__ part, float* __restri
   }
 }
 
-// backward: per-channel mean(dy), mean(dy*y)
-__global__ void bn_bstats_kernel(const double* __restrict__ part, float* __restrict__ mdy, float* __restrict__ mdyy,
-                                 int C, int S, double n) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int s = 0; s < S; ++s) {
-    s1 += part[((size_t)c * S + s) * 2];
-    s2 += part[((size_t)c * S + s) * 2 + 1];
-  }
-  mdy[c] = (float)(s1 / n);
-  mdyy[c] = (float)(s2 / n);
+// backward: per-channel mean(dy), mean(dy*y); one workgroup per channel
+__global__ __launch_bounds__(256) void bn_bstats_kernel(const double* __restrict__ part, float* __restrict__ mdy,
+                                                        float* __restrict__ mdyy, int C, int S, double n) {
+  double s1, s2;
+  bn_combine(part, S, s1, s2);
+  if (threadIdx.x != 0) return;
+  mdy[blockIdx.x] = (float)(s1 / n);
+  mdyy[blockIdx.x] = (float)(s2 / n);
 }
 
 // out = (a - u[c]) * v[c]                         (forward: y = (x - mean) invstd)
@@ -1623,7 +1704,7 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   if (tdr > 0) {
     a.g = train::class_bands(h, dil, tdr);
     const int gd = (int)std::min<int64_t>((int64_t)a.B * a.g.nband, cu_count());
-    hipLaunchKernelGGL((train::conv3x3d_kernel<19>), dim3(gd), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((train::conv3x3d_kernel<19, 0>), dim3(gd), dim3(512), 0, st, a);
   } else if (c == 19 && !(ke && ke[0] == 'v') && train::tm_rows(c, h, w_, dil) > 0) {
     a.g = train::class_bands(h, dil, train::tm_rows(c, h, w_, dil));
     const int gm = train::tc_grid((int64_t)a.B * a.g.nband);
@@ -1726,7 +1807,7 @@ extern "C" int honk_bn_train_fwd_f32(const float* x, float* y, float* mean, floa
   hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, x, (const float*)nullptr, part,
                      (int)batch, c, (int)hw, S);
   HONK_LAUNCH_CHECK("bn_partial_kernel");
-  hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)cdiv(c, 64)), dim3(64), 0, st, (const double*)part, mean,
+  hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, mean,
                      invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
   HONK_LAUNCH_CHECK("bn_stats_kernel");
   const int64_t total = batch * c * hw;
@@ -1750,7 +1831,7 @@ extern "C" int honk_bn_train_bwd_f32(const float* dy, const float* y, const floa
   float* m = (float*)(part + (size_t)c * S * 2);
   hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, dy, y, part, (int)batch, c, (int)hw, S);
   HONK_LAUNCH_CHECK("bn_partial_kernel");
-  hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)cdiv(c, 64)), dim3(64), 0, st, (const double*)part, m,
+  hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, m,
                      m + c, c, S, (double)batch * (double)hw);
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;
@@ -1773,7 +1854,7 @@ extern "C" int honk_res_tail_fwd_f32(const float* h, const float* old, float* s,
   double* part = (double*)workspace;
   hipLaunchKernelGGL(train::tail_partial_kernel, dim3(c, S), dim3(256), 0, st, h, old, part, (int)batch, c, (int)hw, S);
   HONK_LAUNCH_CHECK("tail_partial_kernel");
-  hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)cdiv(c, 64)), dim3(64), 0, st, (const double*)part, mean,
+  hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, mean,
                      invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
   HONK_LAUNCH_CHECK("bn_stats_kernel");
   const int64_t total = batch * c * hw;
@@ -1797,7 +1878,94 @@ extern "C" int honk_res_tail_bwd_f32(const float* gy, const float* gs, const flo
   float* m = (float*)(part + (size_t)c * S * 2);
   hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, gy, y, part, (int)batch, c, (int)hw, S);
   HONK_LAUNCH_CHECK("bn_partial_kernel");
-  hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)cdiv(c, 64)), dim3(64), 0, st, (const double*)part, m,
+  hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, m,
+                     m + c, c, S, (double)batch * (double)hw);
+  HONK_LAUNCH_CHECK("bn_bstats_kernel");
+  const int64_t total = batch * c * hw;
+  const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
+  hipLaunchKernelGGL(train::tail_bwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
+                     (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
+  HONK_LAUNCH_CHECK("tail_bwd_kernel");
+  return HONK_OK;
+}
+
+// ---- the statistics epilogue (conv3x3d_kernel MODE 1 / 2) and the tails that take
+// its partial sums instead of their own pass over the tensors ----
+namespace {
+int stats_grid(int64_t batch, int c, int h, int w_, int dil) {
+  if (batch < 1 || c != 19 || h < 1 || w_ < 1 || dil < 1 || dil > 64) return 0;
+  const char* ke = getenv("HONK_TRAIN_CONV");
+  if (ke && (ke[0] == 'v' || ke[0] == 'm')) return 0;
+  const int tdr = train::td_rows(c, h, w_, dil);
+  if (tdr <= 0) return 0;
+  return (int)std::min<int64_t>(batch * train::class_bands(h, dil, tdr).nband, cu_count());
+}
+}  // namespace
+
+extern "C" size_t honk_conv3x3_stats_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil) {
+  const int S = stats_grid(batch, c, h, w_, dil);
+  return S > 0 ? (size_t)c * S * 2 * sizeof(double) + (size_t)4 * c * sizeof(float) : 0;
+}
+
+extern "C" int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
+                                      int32_t w_, int32_t dil, int32_t flip, int32_t mode, const float* aux,
+                                      void* stats, size_t stats_bytes, void* stream) {
+  int rc = tc_check(x, w, y, batch, c, h, w_, dil);
+  if (rc) return rc;
+  if (mode != 1 && mode != 2) return fail(HONK_ERR_ARG, "conv3x3 statistics mode %d (1 or 2)", mode);
+  if (mode == 2 && !aux) return fail(HONK_ERR_ARG, "conv3x3 statistics mode 2 needs the BN output");
+  const int S = stats_grid(batch, c, h, w_, dil);
+  if (S <= 0) return fail(HONK_ERR_UNSUPPORTED, "conv3x3 statistics epilogue: shape outside conv3x3d_kernel");
+  if (!stats || stats_bytes < honk_conv3x3_stats_bytes(batch, c, h, w_, dil))
+    return fail(HONK_ERR_WORKSPACE, "statistics buffer %zu B < required %zu B", stats_bytes,
+                honk_conv3x3_stats_bytes(batch, c, h, w_, dil));
+  train::Conv3Args a;
+  a.x = x; a.w = w; a.y = y;
+  a.B = (int)batch; a.H = h; a.W = w_; a.flip = flip ? 1 : 0;
+  a.g = train::class_bands(h, dil, train::td_rows(c, h, w_, dil));
+  a.aux = aux;
+  a.part = (double*)stats;
+  hipStream_t st = (hipStream_t)stream;
+  TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
+  if (mode == 1) hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((train::conv3x3d_kernel<19, 2>), dim3(S), dim3(512), 0, st, a);
+  tl.done(st);
+  HONK_LAUNCH_CHECK("conv3x3d_kernel");
+  return HONK_OK;
+}
+
+extern "C" int honk_res_tail_fwd_part_f32(const float* h, const float* old, float* s, float* y, float* mean,
+                                          float* invstd, float* running_mean, float* running_var,
+                                          const void* stats, int64_t batch, int32_t c, int32_t hh, int32_t ww,
+                                          int32_t dil, float momentum, float eps, void* stream) {
+  if (!h || !y || !mean || !invstd || !stats || (!running_mean != !running_var))
+    return fail(HONK_ERR_ARG, "null pointer argument");
+  const int S = stats_grid(batch, c, hh, ww, dil);
+  if (S <= 0) return fail(HONK_ERR_UNSUPPORTED, "res tail: no statistics epilogue for this shape");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t hw = (int64_t)hh * ww;
+  hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)stats,
+                     mean, invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
+  HONK_LAUNCH_CHECK("bn_stats_kernel");
+  const int64_t total = batch * c * hw;
+  const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
+  hipLaunchKernelGGL(train::tail_fwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, h, old,
+                     (const float*)mean, (const float*)invstd, y, s, total, c, (int)hw);
+  HONK_LAUNCH_CHECK("tail_fwd_kernel");
+  return HONK_OK;
+}
+
+extern "C" int honk_res_tail_bwd_part_f32(const float* gy, const float* gs, const float* y, const float* invstd,
+                                          const float* h, float* gh, float* gold, void* stats, int64_t batch,
+                                          int32_t c, int32_t hh, int32_t ww, int32_t dil, void* stream) {
+  if (!gy || !y || !invstd || !h || !gh || !stats) return fail(HONK_ERR_ARG, "null pointer argument");
+  const int S = stats_grid(batch, c, hh, ww, dil);
+  if (S <= 0) return fail(HONK_ERR_UNSUPPORTED, "res tail: no statistics epilogue for this shape");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t hw = (int64_t)hh * ww;
+  double* part = (double*)stats;
+  float* m = (float*)(part + (size_t)c * S * 2);
+  hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, m,
                      m + c, c, S, (double)batch * (double)hw);
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;

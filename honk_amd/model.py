@@ -166,6 +166,7 @@ class SpeechResModel(SerializableModule):
     # (honk_amd/conv3x3.py), the mean and the Linear on honk_amd/head_train.py
     def _torch_forward(self, x, native_convs=False):
         x_in, x = x, x.unsqueeze(1)
+        box_in = None
         for i in range(self.n_layers + 1):
             conv = getattr(self, "conv{}".format(i))
             pool = getattr(self, "pool", None)
@@ -181,15 +182,22 @@ class SpeechResModel(SerializableModule):
             if native_convs and i > 0 and _conv3x3.supported(x, conv) and \
                     _conv3x3.bn_supported(x, getattr(self, "bn{}".format(i))):
                 # conv, then relu / residual add / train BatchNorm as one fused tail
-                h = _conv3x3.conv3x3(x, conv.weight, conv.dilation[0])
+                # statistics boxes: the tail's BatchNorm sums come from this conv's epilogue
+                # (forward) and from the next layer's input-gradient conv (backward)
+                d = conv.dilation[0]
+                box = {}
+                old = old_x if i % 2 == 0 else None
+                h = _conv3x3.conv3x3(x, conv.weight, d, old=old, box_out=box, box_in=box_in)
                 bn = getattr(self, "bn{}".format(i))
                 if i % 2 == 0:
                     keep = i + 2 <= self.n_layers  # old_x is read again by layer i + 2
-                    out = _conv3x3.res_tail(h, old_x, bn, keep_s=keep)
+                    out = _conv3x3.res_tail(h, old_x, bn, keep_s=keep, box=box)
                     x, old_x = out if keep else (out, None)
                 else:
-                    x = _conv3x3.res_tail(h, None, bn)
+                    x = _conv3x3.res_tail(h, None, bn, box=box)
+                box_in = box
                 continue
+            box_in = None
             if native_convs and i > 0 and _conv3x3.supported(x, conv):
                 y = F.relu(_conv3x3.conv3x3(x, conv.weight, conv.dilation[0]))
             else:

@@ -245,6 +245,28 @@ int honk_res_tail_bwd_f32(const float* gy, const float* gs, const float* y, cons
                           float* gh, float* gold, int64_t batch, int32_t c, int64_t hw, void* workspace,
                           size_t workspace_bytes, void* stream);
 /*
+ * The tails' statistics computed in the producing conv's epilogue (the 19-map LDS-DMA
+ * kernel's shapes: honk_conv3x3_stats_bytes > 0), so the tails skip their own pass:
+ *   honk_conv3x3_stats_f32 = honk_conv3x3_f32 that also writes per-workgroup partial sums
+ *   into `stats` -- mode 1 (forward conv, aux = old or NULL): of s = relu(y) [+ aux] and
+ *   s*s; mode 2 (input-gradient conv, flip = 1, aux = the BN output y of the layer below):
+ *   of the conv's output gy and gy*aux;
+ *   honk_res_tail_fwd_part_f32 / honk_res_tail_bwd_part_f32 = honk_res_tail_fwd/bwd_f32
+ *   taking those partials (mode 1 / mode 2 of the same shape; the backward also uses the
+ *   buffer's tail as scratch).  Per-lane fp32 sums, then double in a fixed order: the
+ *   statistics agree with the two-pass tails to fp32 rounding (not bit for bit).
+ */
+size_t honk_conv3x3_stats_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil);
+int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
+                           int32_t w_, int32_t dil, int32_t flip, int32_t mode, const float* aux, void* stats,
+                           size_t stats_bytes, void* stream);
+int honk_res_tail_fwd_part_f32(const float* h, const float* old, float* s, float* y, float* mean, float* invstd,
+                               float* running_mean, float* running_var, const void* stats, int64_t batch, int32_t c,
+                               int32_t h_, int32_t w_, int32_t dil, float momentum, float eps, void* stream);
+int honk_res_tail_bwd_part_f32(const float* gy, const float* gs, const float* y, const float* invstd, const float* h,
+                               float* gh, float* gold, void* stats, int64_t batch, int32_t c, int32_t h_, int32_t w_,
+                               int32_t dil, void* stream);
+/*
  * The res stem in training (model.py:104-110 in training: y = relu(conv0(x)), then
  * AvgPool2d((ph, pw)) when the config has res_pool; ph = pw = 1 without pool),
  * replacing the conv0 / relu / avg_pool2d kernels autograd runs and their backward

@@ -68,8 +68,8 @@ def record(dec: Decisions):
         dec.relu.append((y > 0).detach().cpu())
         return y
 
-    def conv3(x, w, d=1):
-        h = orig_conv3(x, w, d)
+    def conv3(x, w, d=1, **kw):
+        h = orig_conv3(x, w, d, **kw)
         dec.relu.append((h > 0).detach().cpu())
         return h
 

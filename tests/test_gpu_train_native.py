@@ -238,3 +238,39 @@ def test_res_stem_matches_float64(B, C, H, W, pool):
     assert _rel(dw, dw64) < 1e-5
     (dw2,) = torch.autograd.grad(hc.stem(x, conv0, pm), conv0.weight, gy)
     assert torch.equal(dw, dw2)  # deterministic
+
+
+@pytest.mark.parametrize("name,n_layers,B", [("res26-narrow", 6, 48), ("res15-narrow", 13, 6)])
+def test_stats_epilogue_step_matches_two_pass(monkeypatch, name, n_layers, B):
+    """The res tails' BatchNorm statistics from the conv epilogues (honk_conv3x3_stats_f32
+    mode 1 in the forward conv, mode 2 in the next layer's input-gradient conv, then
+    honk_res_tail_*_part_f32) vs the two-pass tails (tail_partial / bn_partial over the
+    tensors): one training step, every gradient within 1e-5 relative, the loss within
+    1e-6; the epilogue serves every tail whose conv (forward) or next conv (backward) runs
+    on the LDS-DMA kernel (dilation <= 4), res15-narrow mixing both kinds of layer."""
+    cfg = dict(hm.find_config(name))
+    cfg["n_layers"] = n_layers
+    dil = [2 ** ((i - 1) // 3) if cfg.get("use_dilation") else 1 for i in range(1, n_layers + 1)]  # model.py:93-98
+    want = {"fwd": sum(d <= 4 for d in dil), "bwd": sum(d <= 4 for d in dil[1:])}
+
+    def step(two_pass):
+        torch.manual_seed(3)
+        m = hm.find_model(name)(cfg).to(DEV).train()
+        g = torch.Generator(device=DEV).manual_seed(4)
+        x = torch.randn(B, 101, 40, device=DEV, generator=g)
+        y = torch.randint(0, 12, (B,), device=DEV, generator=g)
+        if two_pass:
+            monkeypatch.setattr(hc, "_stats_buf", lambda *a, **k: None)
+        before = dict(hc.STATS_USED)
+        loss = torch.nn.functional.cross_entropy(m(x), y)
+        loss.backward()
+        used = {k: hc.STATS_USED[k] - before[k] for k in before}
+        monkeypatch.undo()
+        return float(loss), {k: p.grad.clone() for k, p in m.named_parameters()}, used
+
+    l1, g1, used1 = step(False)
+    l2, g2, used2 = step(True)
+    assert used1 == want and used2 == {"fwd": 0, "bwd": 0}
+    assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l2))
+    for k in g1:
+        assert _rel(g1[k], g2[k]) < 1e-5, k
