@@ -258,17 +258,18 @@ def load_traffic(kernel, clips_per_launch, model):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC pass
     (profiles/pmc_<kernel>.json, written by tools/pmc_summary.py), or None when no
     pass was taken for that kernel at this launch size."""
-    p = os.path.join(REPO, "profiles", f"pmc_{kernel}.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        with open(p) as f:
-            d = json.load(f)
-    except Exception:
-        return None
-    if d.get("batch_clips_per_launch") != clips_per_launch or d.get("model") != model:
-        return None
-    return d.get("hbm_bytes_per_launch")
+    for fn in (f"pmc_{kernel}_{model}.json", f"pmc_{kernel}.json"):
+        p = os.path.join(REPO, "profiles", fn)
+        if not os.path.exists(p):
+            continue
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        if d.get("batch_clips_per_launch") == clips_per_launch and d.get("model") == model:
+            return d.get("hbm_bytes_per_launch", d.get("hbm_bytes_per_step"))
+    return None
 
 
 def _res_geometry(cfg):
@@ -441,7 +442,9 @@ def measure_c2(ctx, args):
                          "achieved": round(ach, 2) if ach else None, "peak": round(peak, 1), "unit": "TFLOP/s",
                          "frac": round(ach / peak, 4) if ach else None, "launches": nl,
                          "avg_launch_ms": round(kms / max(nl, 1), 4), "flop_per_launch": kfl / max(nl, 1),
-                         "traffic": None},
+                         "traffic": load_traffic(f"c2_{prec}_convs", B, name),
+                         "traffic_def": "PMC HBM bytes per conv launch (conv1 and conv2 launches pooled, "
+                                        "profiles/pmc_c2_<mode>_convs_cnn-trad-pool2.json)"},
             "parity": _sample_parity(model, cfg, x, y, orc, B),
             "note": PREC_NOTES.get(prec, "")}
     del x
@@ -510,7 +513,10 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
         "final_loss": float(loss.item()),
         "roofline": {"bound": "mfma", "kernel": "whole training step (per-GPU)",
                      "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": load_traffic("train_step", B, name),
+                     "traffic_def": "PMC HBM bytes of every kernel of one training step "
+                                    "(profiles/pmc_train_step_<model>.json)",
                      "flop_per_clip": fl,
                      "flop_def": "2 x (forward + input-grad + weight-grad MACs), conv0 has no input grad"},
         "note": "native kernels: the stem (conv0 + relu + avg-pool, conv0 weight grad), the block convs' "
