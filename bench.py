@@ -316,6 +316,7 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
         dom = max(set(plan), key=plan.count)
         traffic = load_traffic(f"{dom}_sp{sp}", clips, model)
         what = {"block16p_kernel": "fused odd + even layer pair", "block16w_kernel": "weight-stationary layer",
+                "block16l_kernel": "last layer on the pair's streaming machinery, fused channel sums",
                 "block16r_kernel": "row-band layer"}
         kname = (" + ".join(f"honk::res::{k}<..., SP={sp}> x{plan.count(k)} ({what[k]})"
                             for k in sorted(set(plan), key=plan.index))

@@ -8,7 +8,7 @@ NAME=$1; SRC=$2; FILE=${3:-res}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/exp/_var; mkdir -p "$OUT"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -I "$ROOT/include" \
-  -c "$SRC/$FILE.hip" -o "$OUT/${FILE}_$NAME.o"
+  ${HONK_VFLAGS} -c "$SRC/$FILE.hip" -o "$OUT/${FILE}_$NAME.o"
 OBJS=""
 for f in runtime res cnn train mfcc head augment; do
   if [ "$f" = "$FILE" ]; then OBJS="$OBJS $OUT/${FILE}_$NAME.o"; else OBJS="$OBJS $ROOT/honk_amd/_build/$f.o"; fi

@@ -16,6 +16,8 @@ loop (train.py:131-134) runs unchanged.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from honk_amd import _native
@@ -38,6 +40,25 @@ def supported(x, conv) -> bool:
 def _dedicated(C, H, W, d) -> bool:
     """The {19, 45}-map kernels take (C, H, W, d) (host-only query)."""
     return C in CHANNELS and _native.load().honk_conv3x3_check(int(C), int(H), int(W), int(d)) == 0
+
+
+def _dedicated_conv(C, H, W, d) -> bool:
+    """Forward / input-gradient conv on the dedicated kernels: the 19-map MFMA ones.
+    45 maps go to the same-conv path, whose fp32-MFMA implicit GEMM computes the
+    same fmaf chain as the 45-map VALU kernel (bit-identical) 2.5-4.8x faster
+    (exp/train45_ab.py, res8/res15/res26 shapes); HONK_TRAIN_CONV=v keeps the VALU
+    kernel (tests)."""
+    if C == 45 and os.environ.get("HONK_TRAIN_CONV", "") != "v":
+        return False
+    return _dedicated(C, H, W, d)
+
+
+def _dedicated_wgrad(C, H, W, d) -> bool:
+    """Weight gradient on the dedicated kernels wherever they take the shape: for 45
+    maps the VALU kernel beats the same-conv MFMA one on every block shape (res15
+    0.83-1.13 vs 1.14-1.25 ms, res26 0.238 vs 0.264, res8 0.111 vs 0.121 ms per
+    256 clips, exp/train45_ab.py)."""
+    return _dedicated(C, H, W, d)
 
 
 def _same_ws(B, C, H, W, d, device):
@@ -65,7 +86,7 @@ def _conv(x, w, flip, d=1):
     B, C, H, W = x.shape
     y = torch.empty_like(x)
     lib = _native.load()
-    if _dedicated(C, H, W, d):
+    if _dedicated_conv(C, H, W, d):
         _native.check(lib.honk_conv3x3_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W, d, 1 if flip else 0,
                                            _native.stream_handle(x.device)), "honk_conv3x3_f32")
         return y
@@ -80,7 +101,7 @@ def _wgrad(x, dy, d=1):
     B, C, H, W = x.shape
     lib = _native.load()
     dw = torch.empty(C, C, 3, 3, dtype=torch.float32, device=x.device)
-    if _dedicated(C, H, W, d):
+    if _dedicated_wgrad(C, H, W, d):
         nbytes = lib.honk_conv3x3_wgrad_workspace_bytes(B, C, H, W, d)
         ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=x.device)
         _native.check(lib.honk_conv3x3_wgrad_f32(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), B, C, H, W, d,

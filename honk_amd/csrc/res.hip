@@ -872,6 +872,30 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t
   return pp.ok && ppw && pp.ppw <= ppw ? pp : no;
 }
 
+// The last layer on the pair machinery (block16l_kernel: layer A only, fused
+// channel sums), or ok = false: an odd last layer (no residual) of the 45-map
+// class, full 40-pixel rows (the instantiated row pitches), a ring that fits the
+// stream's share of the LDS.  One clip per stream pass: the plan of a 1-clip stream
+// (no A-out ring: NRB = 1 unused slot, no lag).  HONK_LAST_KERNEL=w keeps the
+// weight-stationary kernel (the pair-vs-w bitwise tests).
+static PairPlan last_at(const Layout& L, const honk_res_desc* d, int SP, int i) {
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 1};
+  const char* kenv = getenv("HONK_RES_KERNEL");
+  const char* lenv = getenv("HONK_LAST_KERNEL");
+  if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r')) || (lenv && lenv[0] == 'w')) return no;
+  if (i != L.L || i % 2 == 0 || L.W != 40) return no;
+  // two streams of 2 A waves: one wave per SIMD (bf16 with four streams, two waves per
+  // SIMD at 256 registers, spilled the weights: 3.38 vs 1.65 ms per 4096-clip launch)
+  const int ns = 2;
+  PairPlan pp = plan_pair(L, SP, dil_of(d, i), 1, 1, ns);
+  if (pp.NRA < 2 || pp.ppr != (SP == 2 ? 9 : 4) || pp.ppw > pair_ppw(SP, pp.ppr)) return no;
+  pp.NRB = 1;
+  pp.lag = 0;
+  pp.ns = ns;
+  pp.ok = (long)(pp.NRA + 1) * pp.slotb + 256 + 1024 <= g16p_lds_bytes() / ns;
+  return pp.ok ? pp : no;
+}
+
 template <int NT, int SP>
 static int launch_block16w(const Block16WArgs& a, hipStream_t st) {
   int grid = cu_count();
@@ -996,7 +1020,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
   int rc;
   if (use_w_kernel(L, d, SP)) {
     // weight-stationary kernel: tiles = (clip, dilation class, band of TH class rows), TH per dilation
-    int nbc_last = 0;
+    int parts_last = 0;  // channel-sum partials per clip of the last layer
     for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
       const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
       rc = (SP == 2) ? launch_conv0<__bf16, true, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
@@ -1013,6 +1037,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
             Block16PArgs pa;
             pa.R = R;
+            pa.chsum = nullptr;
             const float* fr = SP == 2 ? packed + L.off_fragx3 : packed + L.off_frag16;
             const size_t fl = SP == 2 ? L.fragx3_floats : L.frag16_floats;
             pa.wA = (const char*)(fr + (size_t)(i - 1) * fl);
@@ -1043,6 +1068,36 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             ++i;  // layer i + 1 done too
             continue;
           }
+          const PairPlan lp = last_at(L, d, SP, i);
+          if (lp.ok) {
+            Block16PArgs pa;
+            pa.R = R;  // the last (odd) layer reads R
+            const float* fr = SP == 2 ? packed + L.off_fragx3 : packed + L.off_frag16;
+            const size_t fl = SP == 2 ? L.fragx3_floats : L.frag16_floats;
+            pa.wA = pa.wB = (const char*)(fr + (size_t)(i - 1) * fl);
+            pa.chunk_bytes = (unsigned)((size_t)n * L.H * L.W * L.CP * 2 * SP);
+            pa.nclips = (int)n;
+            pa.H = L.H;
+            pa.W = L.W;
+            pa.d = dil_of(d, i);
+            pa.lgd = 0;
+            while ((1 << pa.lgd) < pa.d) ++pa.lgd;
+            pa.sB = 1;
+            pa.lag = 0;
+            pa.NRA = lp.NRA;
+            pa.NRB = lp.NRB;
+            pa.slotb = lp.slotb;
+            pa.ppr = lp.ppr;
+            pa.chsum = chsum;
+            TimedLaunch tl(st, layer_flop_per_clip * (double)n);
+            const dim3 gd(grid), bd(128 * lp.ns);
+            if (SP == 2) hipLaunchKernelGGL((block16l_kernel<3, 2, 9, 9, 2>), gd, bd, 0, st, pa);
+            else hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
+            HONK_LAUNCH_CHECK("res block16l_kernel");
+            tl.done(st);
+            parts_last = 2;
+            continue;
+          }
         }
         Block16WArgs a;
         a.in = even ? X : R;
@@ -1064,7 +1119,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         while ((1 << a.lgd) < a.dil) ++a.lgd;
         if ((int64_t)n * a.nbc > 0x7fffffff) return fail(HONK_ERR_ARG, "chunk too large");
         a.ntiles = (int)(n * a.nbc);
-        if (i == L.L) nbc_last = a.nbc;
+        if (i == L.L) parts_last = a.nbc * 4;
         TimedLaunch tl(st, layer_flop_per_clip * (double)n);
         rc = dispatch_block16w(L.NT, SP, a, st);
         tl.done(st);
@@ -1072,7 +1127,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       }
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
-                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * 4, L.H * L.W, L.C, L.CP, L.NL,
+                         packed + L.off_bout, logits + c0 * L.NL, parts_last, L.H * L.W, L.C, L.CP, L.NL,
                          bn_last, bn_last + L.CP);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (weight-stationary)");
     }
@@ -1164,6 +1219,8 @@ int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, i
     if (pair_at(L, d, SP, n, grid, i).ok) {
       put(HONK_KERNEL_PAIR);
       ++i;
+    } else if (last_at(L, d, SP, i).ok) {
+      put(HONK_KERNEL_LAST);
     } else {
       put(HONK_KERNEL_WSTAT);
     }

@@ -245,14 +245,18 @@ def test_res_launch_plan_host_only(monkeypatch):
         return _native.res_launch_plan(m._desc(101, 40), batch, n_cus=256)
 
     monkeypatch.delenv("HONK_RES_KERNEL", raising=False)
-    assert plan("res15", "bf16x3") == ["block16p_kernel"] * 6 + ["block16w_kernel"]
-    assert plan("res15", "bf16x3", batch=3) == ["block16p_kernel"] * 6 + ["block16w_kernel"]
+    monkeypatch.delenv("HONK_LAST_KERNEL", raising=False)
+    assert plan("res15", "bf16x3") == ["block16p_kernel"] * 6 + ["block16l_kernel"]
+    assert plan("res15", "bf16x3", batch=3) == ["block16p_kernel"] * 6 + ["block16l_kernel"]
     assert plan("res26", "bf16x3") == ["block16p_kernel"] * 11 + ["block16w_kernel"] * 2
     assert plan("res8", "bf16x3") == ["block16p_kernel"] * 2 + ["block16w_kernel"] * 2
     assert plan("res15", "f32") == ["block_kernel"] * 13
-    assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16w_kernel"]
+    assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16l_kernel"]
     assert plan("res8", "bf16") == ["block16r_kernel"] * 6  # 13-pixel rows: row-band measured faster
     assert plan("res15-narrow", "bf16x3") == ["block16r_kernel"] * 13
+    monkeypatch.setenv("HONK_LAST_KERNEL", "w")
+    assert plan("res15", "bf16x3") == ["block16p_kernel"] * 6 + ["block16w_kernel"]
+    monkeypatch.delenv("HONK_LAST_KERNEL")
     monkeypatch.setenv("HONK_RES_KERNEL", "w")
     assert plan("res15", "bf16x3") == ["block16w_kernel"] * 13
     monkeypatch.setenv("HONK_RES_KERNEL", "r")

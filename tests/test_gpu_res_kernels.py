@@ -116,6 +116,10 @@ def test_pair_kernel_bitwise_vs_w(monkeypatch, name, override, B, prec):
     params, x = _case(cfg, B, seed=31)
     m = _module(cfg, params, name, prec)
     monkeypatch.setenv("HONK_RES_KERNEL", "p")
+    # the last layer on the weight-stationary kernel in both runs (block16l_kernel sums
+    # in another order: test_last_kernel_*)
+    monkeypatch.setenv("HONK_LAST_KERNEL", "w")
+    assert "block16l_kernel" not in _native.res_launch_plan(m._desc(101, 40), B)
     # the case must really run the pair kernel (else 'p' would compare 'w' with itself)
     assert "block16p_kernel" in _native.res_launch_plan(m._desc(101, 40), B)
     outp = _run(m, x)
@@ -138,4 +142,51 @@ def test_w_kernel_batch_invariance(monkeypatch):
     full = _run(m, x)
     assert np.array_equal(full, np.concatenate([_run(m, x[:4]), _run(m, x[4:])]))
     monkeypatch.setenv("HONK_RES_CHUNK", "3")
+    assert np.array_equal(full, _run(m, x))
+
+
+# the last (odd) layer on the pair machinery (block16l_kernel): res15 and its
+# variants with an odd layer count; bf16 in both stream counts
+LAST_CASES = [("res15", {}, 600), ("res15", dict(n_layers=7), 300), ("res15", dict(n_feature_maps=33), 260),
+              ("res15", dict(use_dilation=False, n_layers=5), 5)]
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("name,override,B", LAST_CASES)
+def test_last_kernel_vs_w(monkeypatch, name, override, B, prec):
+    """block16l_kernel (the last layer with fused channel sums, one clip per stream
+    pass) vs the weight-stationary last layer: the same products and roundings up to
+    the channel sums, which it adds in another (fixed) order -- within fp32 rounding
+    of each other; the oracle bar of the mode."""
+    cfg = dict(ref_configs()[name])
+    cfg.update(override)
+    params, x = _case(cfg, B, seed=37)
+    m = _module(cfg, params, name, prec)
+    plan = _native.res_launch_plan(m._desc(101, 40), B)
+    assert plan[-1] == "block16l_kernel", plan
+    outl = _run(m, x)
+    monkeypatch.setenv("HONK_LAST_KERNEL", "w")
+    assert _native.res_launch_plan(m._desc(101, 40), B)[-1] == "block16w_kernel"
+    outw = _run(m, x)
+    assert np.abs(outl - outw).max() <= 2e-5 * max(1.0, float(np.abs(outw).max()))
+    idx = list(range(0, B, max(1, B // 8)))[:8]
+    ref = orc.forward(params, cfg, x[idx])
+    if prec == "bf16x3":
+        np.testing.assert_allclose(outl[idx], ref, atol=1e-4, rtol=0)
+    else:
+        assert np.abs(outl[idx] - ref).max() <= 0.05
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+def test_last_kernel_batch_invariance(monkeypatch, prec):
+    """Several clips per workgroup stream at different positions: a clip's logits do
+    not depend on the batch around it or on the chunking (bitwise)."""
+    cfg = dict(ref_configs()["res15"])
+    params, x = _case(cfg, 700, seed=41)
+    m = _module(cfg, params, "res15", prec)
+    assert _native.res_launch_plan(m._desc(101, 40), 700)[-1] == "block16l_kernel"
+    full = _run(m, x)
+    assert np.array_equal(full, np.concatenate([_run(m, x[:263]), _run(m, x[263:])]))
+    assert np.array_equal(full[5:9], _run(m, x[5:9]))
+    monkeypatch.setenv("HONK_RES_CHUNK", "300")
     assert np.array_equal(full, _run(m, x))

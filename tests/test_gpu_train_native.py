@@ -175,6 +175,30 @@ def test_conv3x3_mfma_bitwise_vs_valu(monkeypatch, B, H, W, d):
     assert _rel(outs["m"][2], outs["v"][2]) < 1e-5
 
 
+@pytest.mark.parametrize("B,H,W,d", [(3, 101, 40, 1), (2, 101, 40, 8), (2, 101, 40, 16), (4, 50, 20, 1),
+                                     (5, 25, 13, 1), (2, 9, 5, 3)])
+def test_conv3x3_45_mfma_bitwise_vs_valu(monkeypatch, B, H, W, d):
+    """45-map training convs: the default forward / input gradient run on the same-conv
+    path (fp32-MFMA implicit GEMM, k = 9 c + t fmaf chain) -- bit-identical to the
+    45-map VALU kernel (HONK_TRAIN_CONV=v); the weight gradient stays on the VALU kernel."""
+    g = torch.Generator(device=DEV).manual_seed(11 + H + d)
+    x = torch.randn(B, 45, H, W, device=DEV, generator=g)
+    w = torch.randn(45, 45, 3, 3, device=DEV, generator=g) * 0.05
+    outs = {}
+    for k in ("d", "v"):
+        if k == "d":
+            monkeypatch.delenv("HONK_TRAIN_CONV", raising=False)
+        else:
+            monkeypatch.setenv("HONK_TRAIN_CONV", k)
+        assert hc._dedicated_conv(45, H, W, d) == (k == "v" and hc._dedicated(45, H, W, d))
+        outs[k] = (hc._conv(x, w, flip=False, d=d), hc._conv(x, w, flip=True, d=d))
+    if hc._dedicated(45, H, W, d):
+        assert torch.equal(outs["d"][0], outs["v"][0])
+        assert torch.equal(outs["d"][1], outs["v"][1])
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), padding=d, dilation=d)
+    assert _rel(outs["d"][0], ref) < 1e-5
+
+
 @pytest.mark.parametrize("B,C,H,W,res,keep", [(64, 19, 50, 20, True, True), (64, 19, 50, 20, False, False),
                                               (5, 45, 25, 13, True, False), (3, 19, 101, 40, True, True),
                                               (2, 19, 7, 5, False, False)])
