@@ -77,8 +77,11 @@ def warn_fallback(model, what):
         return
     _warned.add(key)
     import warnings
-    warnings.warn(f"honk_amd: {type(model).__name__} training falls back to PyTorch/MIOpen for {what}",
-                  RuntimeWarning, stacklevel=3)
+    if what.startswith("the eval forward"):
+        msg = f"honk_amd: {type(model).__name__}: {what}"
+    else:
+        msg = f"honk_amd: {type(model).__name__} training falls back to PyTorch/MIOpen for {what}"
+    warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
 def _conv(x, w, flip, d=1):
@@ -351,7 +354,7 @@ def stem_supported(x, conv0, pool) -> bool:
         return False
     if not (tuple(conv0.kernel_size) == (3, 3) and tuple(conv0.padding) == (1, 1) and conv0.bias is None
             and tuple(conv0.stride) == (1, 1) and tuple(conv0.dilation) == (1, 1) and conv0.in_channels == 1
-            and 1 <= conv0.out_channels <= 64 and (x.shape[1] + 2) * (x.shape[2] + 2) <= 8192):
+            and conv0.out_channels >= 1 and (x.shape[1] + 2) * (x.shape[2] + 2) <= 8192):
         return False
     if pool is None:
         return True
@@ -368,4 +371,9 @@ def stem(x, conv0, pool=None):
         ph = pw = 1
     else:
         ph, pw = pool.kernel_size if isinstance(pool.kernel_size, tuple) else (pool.kernel_size,) * 2
-    return _Stem.apply(x, conv0.weight, int(ph), int(pw))
+    w0 = conv0.weight
+    if w0.shape[0] <= 64:
+        return _Stem.apply(x, w0, int(ph), int(pw))
+    # the kernel takes up to 64 output channels: independent channel groups (each
+    # group's weight gradient is its slice of conv0's)
+    return torch.cat([_Stem.apply(x, w0[c:c + 64], int(ph), int(pw)) for c in range(0, w0.shape[0], 64)], 1)

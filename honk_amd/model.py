@@ -287,8 +287,29 @@ class SpeechResModel(SerializableModule):
                           "honk_res_forward")
         return out
 
+    def _native_fits(self, x):
+        """None if the packed forward (honk_res_forward) takes this model and input shape,
+        else the library's reason (host-only queries, cached per precision and map size)."""
+        key = (self.honk_precision, x.shape[1], x.shape[2])
+        fits = self.__dict__.setdefault("_honk_fits", {})
+        if key not in fits:
+            lib = _native.load()
+            desc = self._desc(x.shape[1], x.shape[2])
+            ok = lib.honk_res_packed_floats(desc) != 0 and lib.honk_res_workspace_bytes(desc, 1) != 0
+            fits[key] = None if ok else lib.honk_last_error().decode(errors="replace")
+        return fits[key]
+
     def forward(self, x):
         if _native_ready(x, self):
+            why = self._native_fits(x) if x.dim() == 3 else None
+            if why is not None:
+                # beyond the packed kernels' envelope (more than 64 maps in f32 / 48 in bf16,
+                # maps wider than the bf16 staging plan): the same forward on the layer-level
+                # kernels (native stem, block convs, mean, Linear; eval BatchNorm and the
+                # residual adds as device elementwise ops), in fp32
+                _conv3x3.warn_fallback(self, f"the eval forward of {tuple(x.shape[1:])} inputs in "
+                                             f"{self.honk_precision} ({why}): layer-level fp32 kernels instead")
+                return self._torch_forward(x, native_convs=True)
             return self._native_forward(x)
         return self._torch_forward(x, native_convs=x.is_cuda and self.honk_native_train)
 

@@ -81,18 +81,21 @@ def test_res_config_overrides(override):
     np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=ATOL, rtol=0)
 
 
-def test_res_unsupported_width_fails_loudly():
-    """Beyond the kernels' envelope the forward raises (no silent fallback): more than
-    64 maps in f32, more than 48 in bf16 / bf16x3."""
-    cfg = dict(ref_configs()["res8"], n_feature_maps=65)
-    m = hm.find_model("res8")(cfg).eval().to(DEV)
-    with pytest.raises(RuntimeError, match="64 maps"):
-        m(torch.zeros(1, 101, 40, device=DEV))
-    cfg = dict(ref_configs()["res8"], n_feature_maps=64)
-    m = hm.find_model("res8")(cfg).eval().to(DEV)
-    m.honk_precision = "bf16x3"
-    with pytest.raises(RuntimeError, match="48 in bf16"):
-        m(torch.zeros(1, 101, 40, device=DEV))
+def test_res_wide_models_run_on_layer_kernels():
+    """Beyond the packed forward's envelope (more than 64 maps in f32, more than 48 in
+    bf16 / bf16x3) the C-ABI refuses the descriptor (HONK_ERR_UNSUPPORTED, no silent
+    fallback there) and the module says so once (RuntimeWarning) and runs the same
+    forward on the layer-level fp32 kernels: oracle parity at the fp32 bar."""
+    for maps, prec in ((65, "f32"), (96, "f32"), (64, "bf16x3"), (49, "bf16")):
+        cfg = dict(ref_configs()["res8"], n_feature_maps=maps)
+        params, x = _res_case(cfg, 3, seed=maps)
+        m = module(cfg, params, "res8")
+        m.honk_precision = prec
+        assert _native.load().honk_res_packed_floats(m._desc(101, 40)) == 0 or \
+            _native.load().honk_res_workspace_bytes(m._desc(101, 40), 1) == 0
+        with pytest.warns(RuntimeWarning, match="layer-level fp32 kernels"):
+            out = run(m, x)
+        np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=ATOL, rtol=0)
 
 
 @pytest.mark.parametrize("name,B", [("cnn-trad-pool2", 3), ("cnn-one-fstride4", 5), ("cnn-tpool2", 2),
@@ -250,8 +253,12 @@ def test_res_wide_input_envelope(width, prec, ok):
     m = module(cfg, params, "res15")
     m.honk_precision = prec
     if not ok:
-        with pytest.raises(RuntimeError, match="row-band staging plan"):
-            run(m, x)
+        # the packed forward refuses; the module runs the layer-level fp32 kernels
+        assert _native.load().honk_res_workspace_bytes(m._desc(101, width), 1) == 0
+        assert "row-band staging plan" in _native.load().honk_last_error().decode()
+        with pytest.warns(RuntimeWarning, match="layer-level fp32 kernels"):
+            out = run(m, x)
+        np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=ATOL, rtol=0)
         return
     tol = 5e-2 if prec == "bf16" else ATOL
     np.testing.assert_allclose(run(m, x), orc.forward(params, cfg, x), atol=tol, rtol=0)
