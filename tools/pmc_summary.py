@@ -34,7 +34,7 @@ def per_kernel(path, counter):
 
 # kernel families: a family pools every template instance of the named kernels
 # (weighted by launches); the bf16 res kernels are split by SP (sp1 = bf16, sp2 = bf16x3)
-SP_ARG = {"block16r_kernel": 2, "block16w_kernel": 1, "block16p_kernel": 1}
+SP_ARG = {"block16r_kernel": 2, "block16w_kernel": 1, "block16p_kernel": 1, "block16l_kernel": 1}
 POOLS = {"block_kernel": ("block_kernel",), "conv_gemm_kernel": ("conv_gemm_kernel",),
          "c2_f32_convs": ("conv1f_kernel", "conv2f_kernel"),
          "c2_bf16x3_convs": ("conv1x3_kernel", "conv2x3_kernel"),
