@@ -88,6 +88,13 @@ _PROTOS = {
     "honk_conv3x3_stats_bytes": (ctypes.c_size_t, [ctypes.c_int64] + [ctypes.c_int32] * 4),
     "honk_conv3x3_stats_f32": (ctypes.c_int, [c_f32p] * 3 + [ctypes.c_int64] + [ctypes.c_int32] * 6
                                + [c_f32p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_conv3x3_tail_f32": (ctypes.c_int, [c_f32p] * 3 + [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_int32] * 4
+                              + [c_f32p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_res_tail_fwd_s_f32": (ctypes.c_int, [c_f32p] * 6 + [ctypes.c_void_p, ctypes.c_int64]
+                                + [ctypes.c_int32] * 4 + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]),
+    "honk_res_tail_bwd_mask_f32": (ctypes.c_int, [c_f32p] * 4 + [ctypes.c_void_p] + [c_f32p] * 2
+                                   + [ctypes.c_int64] + [ctypes.c_int32] * 4
+                                   + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "honk_res_tail_fwd_part_f32": (ctypes.c_int, [c_f32p] * 8 + [ctypes.c_void_p, ctypes.c_int64]
                                    + [ctypes.c_int32] * 4 + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]),
     "honk_res_tail_bwd_part_f32": (ctypes.c_int, [c_f32p] * 7 + [ctypes.c_void_p, ctypes.c_int64]

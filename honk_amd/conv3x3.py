@@ -138,12 +138,18 @@ def _conv_stats(x, w, flip, d, mode, aux, buf):
     return y
 
 
+FUSE_TAIL = os.environ.get("HONK_TRAIN_FUSE_TAIL", "1") != "0"   # tests compare both
+
+
 class _Conv3x3(torch.autograd.Function):
     """h = conv(x, w).  Statistics boxes (dicts shared with honk_amd's res tails, see
     res_tail): box_out -> this conv's epilogue also sums the next tail's forward
-    statistics (of relu(h) [+ old]) into box_out["fwd"]; box_in (the box of the tail
-    whose output x is) -> the input-gradient conv sums that tail's backward statistics
-    (of dx and dx * x) into box_in["bwd"] = (buffer, dx)."""
+    statistics (of relu(h) [+ old]) into box_out["fwd"], and (FUSE_TAIL) writes the
+    tail's s = relu(h) [+ old] in place of h plus the ReLU mask (box_out["mask"]): the
+    returned tensor then holds s, which only the tail reads (autograd still sees h: the
+    gradient it hands back is the tail's gh); box_in (the box of the tail whose output x
+    is) -> the input-gradient conv sums that tail's backward statistics (of dx and
+    dx * x) into box_in["bwd"] = (buffer, dx)."""
 
     @staticmethod
     def forward(ctx, x, w, d, old, box_out, box_in):
@@ -156,7 +162,18 @@ class _Conv3x3(torch.autograd.Function):
             buf = _stats_buf(B, C, H, W, d, x.device)
             if buf is not None:
                 box_out["fwd"] = (buf, d)   # partials laid out by this conv's grid (its dilation)
-                return _conv_stats(x, w, False, d, 1, old.contiguous() if old is not None else None, buf)
+                oc = old.contiguous() if old is not None else None
+                if FUSE_TAIL:
+                    x = x.contiguous()
+                    s = torch.empty_like(x)
+                    mask = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+                    _native.check(_native.load().honk_conv3x3_tail_f32(
+                        x.data_ptr(), w.data_ptr(), s.data_ptr(), mask.data_ptr(), B, C, H, W, d,
+                        oc.data_ptr() if oc is not None else None, buf.data_ptr(), buf.numel(),
+                        _native.stream_handle(x.device)), "honk_conv3x3_tail_f32")
+                    box_out["mask"] = mask
+                    return s
+                return _conv_stats(x, w, False, d, 1, oc, buf)
         return _conv(x, w, flip=False, d=d)
 
     @staticmethod
@@ -231,11 +248,26 @@ class _ResTail(torch.autograd.Function):
         old = old.contiguous() if old is not None else None
         B, C, H, W = h.shape
         y = torch.empty_like(h)
-        s = torch.empty_like(h) if keep_s else None
         mean = torch.empty(C, dtype=torch.float32, device=h.device)
         invstd = torch.empty_like(mean)
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         st = _native.stream_handle(h.device)
+        mask = box.pop("mask", None) if box is not None else None
+        if mask is not None:
+            # h holds s = relu(h) [+ old] from the conv's epilogue (and old was read there)
+            STATS_USED["fwd"] += 1
+            buf, d = box.pop("fwd")
+            _native.check(_native.load().honk_res_tail_fwd_s_f32(
+                h.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean), ptr(running_var),
+                buf.data_ptr(), B, C, H, W, d, momentum, eps, st), "honk_res_tail_fwd_s_f32")
+            ctx.save_for_backward(mask, y, invstd)
+            ctx.has_old = old is not None
+            ctx.box = box
+            ctx.masked = True
+            if keep_s:
+                return y, h
+            return y
+        s = torch.empty_like(h) if keep_s else None
         if box is not None and "fwd" in box:
             STATS_USED["fwd"] += 1
             buf, d = box.pop("fwd")
@@ -251,13 +283,14 @@ class _ResTail(torch.autograd.Function):
         ctx.save_for_backward(h, y, invstd)
         ctx.has_old = old is not None
         ctx.box = box
+        ctx.masked = False
         if keep_s:
             return y, s
         return y
 
     @staticmethod
     def backward(ctx, gy, gs=None):
-        h, y, invstd = ctx.saved_tensors
+        h, y, invstd = ctx.saved_tensors  # (masked: h is the conv epilogue's ReLU mask)
         B, C, H, W = y.shape
         if gy is None:
             gy = torch.zeros_like(y)
@@ -267,7 +300,18 @@ class _ResTail(torch.autograd.Function):
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         st = _native.stream_handle(y.device)
         pre = ctx.box.pop("bwd", None) if ctx.box is not None else None
-        if pre is not None and pre[1] is gy and gy._version == pre[2]:
+        if ctx.masked:
+            if pre is not None and pre[1] is gy and gy._version == pre[2]:
+                STATS_USED["bwd"] += 1
+                buf, dil = pre[0], pre[3]
+            else:  # no input-gradient conv summed this gradient's statistics: the tail does
+                gy = gy.contiguous()
+                buf, _ = _bn_ws(B, C, H * W, y.device)
+                dil = 0
+            _native.check(_native.load().honk_res_tail_bwd_mask_f32(
+                gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(), h.data_ptr(), gh.data_ptr(), ptr(gold),
+                B, C, H, W, dil, buf.data_ptr(), buf.numel(), st), "honk_res_tail_bwd_mask_f32")
+        elif pre is not None and pre[1] is gy and gy._version == pre[2]:
             # the statistics of exactly this gradient, summed by the conv that produced it
             STATS_USED["bwd"] += 1
             _native.check(_native.load().honk_res_tail_bwd_part_f32(

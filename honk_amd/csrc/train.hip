@@ -123,6 +123,9 @@ struct Conv3Args {
   // conv3x3d_kernel's BatchNorm statistics epilogue (MODE 1 / 2), else unused:
   const float* aux;  // MODE 1: the residual old (may be null); MODE 2: the BN output y
   double* part;      // [C][gridDim.x][2] per-workgroup partial sums
+  // MODE 1 only, may be null: y receives s = relu(conv) [+ aux] instead of conv, and
+  // mask[i] = !(conv <= 0) (the ReLU's backward mask, torch's threshold_backward)
+  unsigned char* mask;
 };
 
 typedef float tf2 __attribute__((ext_vector_type(2)));
@@ -520,6 +523,45 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
   float sa[MODE ? C : 1], sb[MODE ? C : 1];  // per-lane statistics (MODE 1 / 2)
 #pragma unroll
   for (int o = 0; o < (MODE ? C : 1); ++o) sa[o] = sb[o] = 0.f;
+  // Deferred epilogue: a super tile's outputs (stores, statistics) go out during the
+  // MFMAs of the wave's next super tile -- one channel every 8 k -- instead of after
+  // its own loop, where the 8 waves (one super tile each per band tile) would all sit
+  // in their epilogues together with the matrix pipes idle.  Per lane the super tiles
+  // and channels are still summed in the same order: bit-identical statistics.
+  f32x4_t pacc[NG];  // the pending super tile's accumulators
+  float pav[MODE ? C : 1];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) pacc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int o = 0; o < (MODE ? C : 1); ++o) pav[o] = 0.f;
+  float* pyb = a.y;
+  size_t ppix = 0;
+  bool ppv = false;  // the pending super tile has a valid pixel in this lane
+  auto epi = [&](int o) {
+    if (o < C && ppv) {
+      const float v = pacc[o >> 2][o & 3];
+      if constexpr (MODE == 1) {
+        float sv = v <= 0.f ? 0.f : v;  // relu_f: NaN passes, as torch.relu
+        if (a.aux) sv = sv + pav[o];
+        if (a.mask) {
+          pyb[(size_t)o * H * W + ppix] = sv;
+          a.mask[(size_t)(pyb - a.y) + (size_t)o * H * W + ppix] = v <= 0.f ? 0 : 1;
+        } else {
+          pyb[(size_t)o * H * W + ppix] = v;
+        }
+        sa[o] += sv;
+        sb[o] += sv * sv;
+      } else {
+        pyb[(size_t)o * H * W + ppix] = v;
+      }
+      if constexpr (MODE == 2) {
+        sa[o] += v;
+        sb[o] += v * pav[o];
+      }
+    }
+  };
+  constexpr int EK0 = 4, EKS = 8;  // channel o's epilogue at k = EK0 + EKS o
+  static_assert(EK0 + EKS * (C - 1) < K, "epilogue inside the k loop");
   float* buf0 = tdl;
   float* buf1 = tdl + TD_BUF / 4;
   if ((int)blockIdx.x < ntile) issue(blockIdx.x, buf0);
@@ -543,8 +585,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
       f32x4_t acc[NG];
 #pragma unroll
       for (int g = 0; g < NG; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      // the statistics epilogue's operand (old / y at this lane's pixel), read before the
-      // MFMAs so its latency hides behind them
+      // the statistics epilogue's operand (old / y at this lane's pixel), read now: it is
+      // used a whole super tile later
       float av[MODE ? C : 1];
       const size_t pix = (size_t)(r + (k0 + j) * d) * W + col;
       if constexpr (MODE != 0) {
@@ -555,42 +597,36 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
       float xr[PF];  // ring of operands read PF k ahead (PF divides 16: slots are compile-time)
 #pragma unroll
       for (int k = 0; k < PF; ++k) xr[k] = xp[kof(k)];
-#pragma unroll
-      for (int jj = 0; jj < KT; ++jj)
+      static_for<KT>([&](auto jc) {
+        constexpr int JJ = decltype(jc)::value;
         static_for<16>([&](auto bc) {
           constexpr int B = decltype(bc)::value;
-          const int k = 16 * jj + B;
-          if (k < K) {
+          constexpr int k = 16 * JJ + B;
+          if constexpr (k < K) {
             const float xv = xr[B % PF];
             xr[B % PF] = xp[kof(k + PF < K ? k + PF : K - 1)];
 #pragma unroll
-            for (int g = 0; g < NG; ++g) acc[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(wt[g][jj], xv, acc[g], 4, B, 0);
+            for (int g = 0; g < NG; ++g) acc[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(wt[g][JJ], xv, acc[g], 4, B, 0);
+            if constexpr (k >= EK0 && (k - EK0) % EKS == 0 && (k - EK0) / EKS < C) epi((k - EK0) / EKS);
             __builtin_amdgcn_sched_barrier(0);  // keeps each read PF k ahead of its use
           }
         });
-      if (pv) {
+      });
+      // this super tile becomes the pending one
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
+      for (int g = 0; g < NG; ++g) pacc[g] = acc[g];
+      if constexpr (MODE != 0) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int o = 4 * g + i;
-            if (o < C) {
-              const float v = acc[g][i];
-              yb[(size_t)o * H * W + pix] = v;
-              if constexpr (MODE == 1) {
-                float sv = v <= 0.f ? 0.f : v;  // relu_f: NaN passes, as torch.relu
-                if (a.aux) sv = sv + av[o];
-                sa[o] += sv;
-                sb[o] += sv * sv;
-              } else if constexpr (MODE == 2) {
-                sa[o] += v;
-                sb[o] += v * av[o];
-              }
-            }
-          }
+        for (int o = 0; o < C; ++o) pav[o] = av[o];
       }
+      pyb = yb;
+      ppix = pix;
+      ppv = pv;
     }
   }
+  // the last super tile's epilogue
+#pragma unroll
+  for (int o = 0; o < C; ++o) epi(o);
   td_wait_vm0();  // no DMA left in flight when the workgroup retires
   if constexpr (MODE != 0) {
     __shared__ double red[8][C][2];
@@ -1334,6 +1370,8 @@ __global__ __launch_bounds__(256) void tail_partial_kernel(const float* __restri
 }
 
 // y = (relu(h) [+ old] - mean[c]) * invstd[c]; s_out (may be null) = relu(h) [+ old]
+// (s_in: h already holds s = relu(h) [+ old], made by the conv's epilogue: y = (h - mean) * invstd)
+template <bool S_IN>
 __global__ __launch_bounds__(256) void tail_fwd_kernel(const float* __restrict__ h, const float* __restrict__ old,
                                                        const float* __restrict__ u, const float* __restrict__ v,
                                                        float* __restrict__ y, float* __restrict__ s_out, int64_t total,
@@ -1344,6 +1382,10 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const float* __restrict__
     if (i4 >= total) return;
     const int c = (int)((i4 / HW) % C);
     const float4 hv = *(const float4*)(h + i4);
+    if constexpr (S_IN) {
+      *(float4*)(y + i4) = float4{(hv.x - u[c]) * v[c], (hv.y - u[c]) * v[c], (hv.z - u[c]) * v[c], (hv.w - u[c]) * v[c]};
+      return;
+    }
     float4 a = float4{relu_f(hv.x), relu_f(hv.y), relu_f(hv.z), relu_f(hv.w)};
     if (old) {
       const float4 ov = *(const float4*)(old + i4);
@@ -1355,6 +1397,10 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const float* __restrict__
   }
   if (i >= total) return;
   const int c = (int)((i / HW) % C);
+  if constexpr (S_IN) {
+    y[i] = (h[i] - u[c]) * v[c];
+    return;
+  }
   float a = relu_f(h[i]);
   if (old) a = a + old[i];
   if (s_out) s_out[i] = a;
@@ -1362,17 +1408,29 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const float* __restrict__
 }
 
 // g = v[c] (gy - u[c] - y w[c]) [+ gs]; gold (may be null) = g; gh = h > 0 ? g : 0
+// (MASK: the conv epilogue's byte mask !(h <= 0) in place of h)
+template <bool MASK>
 __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ y,
-                                                       const float* __restrict__ gs, const float* __restrict__ h,
+                                                       const float* __restrict__ gs, const void* __restrict__ hm,
                                                        const float* __restrict__ u, const float* __restrict__ v,
                                                        const float* __restrict__ w, float* __restrict__ gh,
                                                        float* __restrict__ gold, int64_t total, int C, int HW) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float* h = (const float*)hm;
+  const unsigned char* mk = (const unsigned char*)hm;
   if ((HW & 3) == 0) {
     const int64_t i4 = 4 * i;
     if (i4 >= total) return;
     const int c = (int)((i4 / HW) % C);
-    const float4 av = *(const float4*)(gy + i4), bv = *(const float4*)(y + i4), hv = *(const float4*)(h + i4);
+    const float4 av = *(const float4*)(gy + i4), bv = *(const float4*)(y + i4);
+    float4 hv;
+    if constexpr (MASK) {
+      const unsigned mw = *(const unsigned*)(mk + i4);  // 4 mask bytes: 1 = h > 0 (or NaN)
+      hv = float4{(mw & 0xffu) ? 1.f : 0.f, (mw & 0xff00u) ? 1.f : 0.f, (mw & 0xff0000u) ? 1.f : 0.f,
+                  (mw & 0xff000000u) ? 1.f : 0.f};
+    } else {
+      hv = *(const float4*)(h + i4);
+    }
     float4 g = float4{v[c] * (av.x - u[c] - bv.x * w[c]), v[c] * (av.y - u[c] - bv.y * w[c]),
                       v[c] * (av.z - u[c] - bv.z * w[c]), v[c] * (av.w - u[c] - bv.w * w[c])};
     if (gs) {
@@ -1389,7 +1447,8 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__
   float g = v[c] * (gy[i] - u[c] - y[i] * w[c]);
   if (gs) g = g + gs[i];
   if (gold) gold[i] = g;
-  gh[i] = h[i] <= 0.f ? 0.f : g;
+  if constexpr (MASK) gh[i] = mk[i] ? g : 0.f;
+  else gh[i] = h[i] <= 0.f ? 0.f : g;
 }
 
 // ---------------------------------------------------------------------------- //
@@ -1859,7 +1918,7 @@ extern "C" int honk_res_tail_fwd_f32(const float* h, const float* old, float* s,
   HONK_LAUNCH_CHECK("bn_stats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
-  hipLaunchKernelGGL(train::tail_fwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, h, old,
+  hipLaunchKernelGGL(train::tail_fwd_kernel<false>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, h, old,
                      (const float*)mean, (const float*)invstd, y, s, total, c, (int)hw);
   HONK_LAUNCH_CHECK("tail_fwd_kernel");
   return HONK_OK;
@@ -1883,7 +1942,7 @@ extern "C" int honk_res_tail_bwd_f32(const float* gy, const float* gs, const flo
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
-  hipLaunchKernelGGL(train::tail_bwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
+  hipLaunchKernelGGL(train::tail_bwd_kernel<false>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
                      (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
   HONK_LAUNCH_CHECK("tail_bwd_kernel");
   return HONK_OK;
@@ -1925,12 +1984,97 @@ extern "C" int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, 
   a.g = train::class_bands(h, dil, train::td_rows(c, h, w_, dil));
   a.aux = aux;
   a.part = (double*)stats;
+  a.mask = nullptr;
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
   if (mode == 1) hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((train::conv3x3d_kernel<19, 2>), dim3(S), dim3(512), 0, st, a);
   tl.done(st);
   HONK_LAUNCH_CHECK("conv3x3d_kernel");
+  return HONK_OK;
+}
+
+extern "C" int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, unsigned char* mask, int64_t batch,
+                                     int32_t c, int32_t h, int32_t w_, int32_t dil, const float* old, void* stats,
+                                     size_t stats_bytes, void* stream) {
+  int rc = tc_check(x, w, s, batch, c, h, w_, dil);
+  if (rc) return rc;
+  if (!mask) return fail(HONK_ERR_ARG, "null pointer argument");
+  const int S = stats_grid(batch, c, h, w_, dil);
+  if (S <= 0) return fail(HONK_ERR_UNSUPPORTED, "conv3x3 tail epilogue: shape outside conv3x3d_kernel");
+  if (!stats || stats_bytes < honk_conv3x3_stats_bytes(batch, c, h, w_, dil))
+    return fail(HONK_ERR_WORKSPACE, "statistics buffer %zu B < required %zu B", stats_bytes,
+                honk_conv3x3_stats_bytes(batch, c, h, w_, dil));
+  train::Conv3Args a;
+  a.x = x; a.w = w; a.y = s;
+  a.B = (int)batch; a.H = h; a.W = w_; a.flip = 0;
+  a.g = train::class_bands(h, dil, train::td_rows(c, h, w_, dil));
+  a.aux = old;
+  a.part = (double*)stats;
+  a.mask = mask;
+  hipStream_t st = (hipStream_t)stream;
+  TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
+  hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
+  tl.done(st);
+  HONK_LAUNCH_CHECK("conv3x3d_kernel (tail epilogue)");
+  return HONK_OK;
+}
+
+extern "C" int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, float* invstd, float* running_mean,
+                                       float* running_var, const void* stats, int64_t batch, int32_t c, int32_t hh,
+                                       int32_t ww, int32_t dil, float momentum, float eps, void* stream) {
+  if (!s || !y || !mean || !invstd || !stats || (!running_mean != !running_var))
+    return fail(HONK_ERR_ARG, "null pointer argument");
+  const int S = stats_grid(batch, c, hh, ww, dil);
+  if (S <= 0) return fail(HONK_ERR_UNSUPPORTED, "res tail: no statistics epilogue for this shape");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t hw = (int64_t)hh * ww;
+  hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)stats,
+                     mean, invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
+  HONK_LAUNCH_CHECK("bn_stats_kernel");
+  const int64_t total = batch * c * hw;
+  const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
+  hipLaunchKernelGGL(train::tail_fwd_kernel<true>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, s,
+                     (const float*)nullptr, (const float*)mean, (const float*)invstd, y, (float*)nullptr, total, c,
+                     (int)hw);
+  HONK_LAUNCH_CHECK("tail_fwd_kernel");
+  return HONK_OK;
+}
+
+extern "C" int honk_res_tail_bwd_mask_f32(const float* gy, const float* gs, const float* y, const float* invstd,
+                                          const unsigned char* mask, float* gh, float* gold, int64_t batch, int32_t c,
+                                          int32_t hh, int32_t ww, int32_t dil, void* stats, size_t stats_bytes,
+                                          void* stream) {
+  if (!gy || !y || !invstd || !mask || !gh || !stats) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 1 || c < 1 || hh < 1 || ww < 1 || batch > 0x7fffffff || (int64_t)hh * ww > 0x7fffffff)
+    return fail(HONK_ERR_ARG, "bad res tail shape");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t hw = (int64_t)hh * ww;
+  double* part = (double*)stats;
+  int S;
+  if (dil > 0) {  // the input-gradient conv's epilogue summed them (its grid's partials)
+    S = stats_grid(batch, c, hh, ww, dil);
+    if (S <= 0) return fail(HONK_ERR_UNSUPPORTED, "res tail: no statistics epilogue for this shape");
+    if (stats_bytes < honk_conv3x3_stats_bytes(batch, c, hh, ww, dil))
+      return fail(HONK_ERR_WORKSPACE, "statistics buffer %zu B < required %zu B", stats_bytes,
+                  honk_conv3x3_stats_bytes(batch, c, hh, ww, dil));
+  } else {  // dil = 0: no conv consumed the gradient (the last block): sum them here
+    const size_t need = honk_bn_train_workspace_bytes(batch, c, hw);
+    if (stats_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", stats_bytes, need);
+    S = train::bn_slices((int)batch, c);
+    hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, gy, y, part, (int)batch, c, (int)hw,
+                       S);
+    HONK_LAUNCH_CHECK("bn_partial_kernel");
+  }
+  float* m = (float*)(part + (size_t)c * S * 2);
+  hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, m,
+                     m + c, c, S, (double)batch * (double)hw);
+  HONK_LAUNCH_CHECK("bn_bstats_kernel");
+  const int64_t total = batch * c * hw;
+  const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
+  hipLaunchKernelGGL(train::tail_bwd_kernel<true>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs,
+                     (const void*)mask, (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
+  HONK_LAUNCH_CHECK("tail_bwd_kernel");
   return HONK_OK;
 }
 
@@ -1949,7 +2093,7 @@ extern "C" int honk_res_tail_fwd_part_f32(const float* h, const float* old, floa
   HONK_LAUNCH_CHECK("bn_stats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
-  hipLaunchKernelGGL(train::tail_fwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, h, old,
+  hipLaunchKernelGGL(train::tail_fwd_kernel<false>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, h, old,
                      (const float*)mean, (const float*)invstd, y, s, total, c, (int)hw);
   HONK_LAUNCH_CHECK("tail_fwd_kernel");
   return HONK_OK;
@@ -1970,7 +2114,7 @@ extern "C" int honk_res_tail_bwd_part_f32(const float* gy, const float* gs, cons
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
-  hipLaunchKernelGGL(train::tail_bwd_kernel, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
+  hipLaunchKernelGGL(train::tail_bwd_kernel<false>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
                      (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
   HONK_LAUNCH_CHECK("tail_bwd_kernel");
   return HONK_OK;

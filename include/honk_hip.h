@@ -257,6 +257,29 @@ int honk_res_tail_bwd_f32(const float* gy, const float* gs, const float* y, cons
  *   buffer's tail as scratch).  Per-lane fp32 sums, then double in a fixed order: the
  *   statistics agree with the two-pass tails to fp32 rounding (not bit for bit).
  */
+/*
+ * The forward conv of a res block with the tail's elementwise head in its epilogue (the
+ * statistics epilogue's shapes): s = relu(conv(x, w)) [+ old] is written instead of the
+ * conv output (NCHW, as x), mask[i] = !(conv <= 0) (one byte per element: the ReLU's
+ * backward mask, NaN counts as > 0 as in torch's threshold_backward), and the statistics
+ * of s as honk_conv3x3_stats_f32 mode 1.  Then honk_res_tail_fwd_s_f32 makes
+ * y = BatchNorm_train(s) from s alone, and honk_res_tail_bwd_mask_f32 is
+ * honk_res_tail_bwd_part_f32 with the mask in place of the conv output: the tails read
+ * neither the conv output nor old, and write no separate s.  Same fp32 operations as the
+ * unfused tails (bit-identical given the same statistics).
+ */
+int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, unsigned char* mask, int64_t batch, int32_t c,
+                          int32_t h, int32_t w_, int32_t dil, const float* old, void* stats, size_t stats_bytes,
+                          void* stream);
+int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, float* invstd, float* running_mean,
+                            float* running_var, const void* stats, int64_t batch, int32_t c, int32_t hh, int32_t ww,
+                            int32_t dil, float momentum, float eps, void* stream);
+/* dil >= 1: `stats` = the input-gradient conv's partials (honk_conv3x3_stats_f32 mode 2 at
+ * dilation dil); dil = 0: `stats` is a workspace of honk_bn_train_workspace_bytes(batch, c,
+ * hh * ww) and the statistics are summed here (a block whose output feeds no conv). */
+int honk_res_tail_bwd_mask_f32(const float* gy, const float* gs, const float* y, const float* invstd,
+                               const unsigned char* mask, float* gh, float* gold, int64_t batch, int32_t c,
+                               int32_t hh, int32_t ww, int32_t dil, void* stats, size_t stats_bytes, void* stream);
 size_t honk_conv3x3_stats_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil);
 int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
                            int32_t w_, int32_t dil, int32_t flip, int32_t mode, const float* aux, void* stats,

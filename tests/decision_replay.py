@@ -70,7 +70,13 @@ def record(dec: Decisions):
 
     def conv3(x, w, d=1, **kw):
         h = orig_conv3(x, w, d, **kw)
-        dec.relu.append((h > 0).detach().cpu())
+        box = kw.get("box_out")
+        if box is not None and "mask" in box:
+            # the fused tail: the conv's output holds s = relu(h) [+ old]; its epilogue
+            # wrote the ReLU decision itself (!(h <= 0))
+            dec.relu.append(box["mask"].bool().cpu())
+        else:
+            dec.relu.append((h > 0).detach().cpu())
         return h
 
     def stem(x, conv0, pool=None):

@@ -298,3 +298,34 @@ def test_stats_epilogue_step_matches_two_pass(monkeypatch, name, n_layers, B):
     assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l2))
     for k in g1:
         assert _rel(g1[k], g2[k]) < 1e-5, k
+
+
+@pytest.mark.parametrize("name,n_layers,B", [("res26-narrow", 6, 48), ("res15-narrow", 13, 6), ("res26-narrow", 5, 9)])
+def test_fused_tail_step_bitwise(monkeypatch, name, n_layers, B):
+    """The forward conv writing the tail's s = relu(h) [+ old] and the ReLU byte mask
+    (honk_conv3x3_tail_f32, then honk_res_tail_fwd_s_f32 / honk_res_tail_bwd_mask_f32)
+    vs the same statistics epilogue with the tails reading h and old: one training
+    step, bit-identical loss, gradients and running statistics (same fp32 operations);
+    odd and even layer counts (the last tail's backward sums its own statistics)."""
+    cfg = dict(hm.find_config(name))
+    cfg["n_layers"] = n_layers
+
+    def step(fuse):
+        monkeypatch.setattr(hc, "FUSE_TAIL", fuse)
+        torch.manual_seed(3)
+        m = hm.find_model(name)(cfg).to(DEV).train()
+        g = torch.Generator(device=DEV).manual_seed(5)
+        x = torch.randn(B, 101, 40, device=DEV, generator=g)
+        y = torch.randint(0, 12, (B,), device=DEV, generator=g)
+        loss = torch.nn.functional.cross_entropy(m(x), y)
+        loss.backward()
+        bufs = {k: b.clone() for k, b in m.named_buffers()}
+        return loss.detach(), {k: p.grad.clone() for k, p in m.named_parameters()}, bufs
+
+    l1, g1, b1 = step(True)
+    l2, g2, b2 = step(False)
+    assert torch.equal(l1, l2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+    for k in b1:
+        assert torch.equal(b1[k], b2[k]), k
