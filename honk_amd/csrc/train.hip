@@ -461,15 +461,19 @@ __device__ __forceinline__ f32x4_t mfma4_bc(float a, float b, f32x4_t c, int abi
 //   2: the BatchNorm backward statistics of gy = this (input-gradient) conv's output with
 //      the BN output y (bn_partial_kernel's sums: gy and gy*y).
 // Per lane fp32 sums over its pixels, then double across lanes and waves.
-template <int C, int MODE>
+// FW, FD, FTH (all > 0): the tile geometry (map width, dilation, class rows per tile)
+// fixed at compile time, so every k's operand offset is an immediate of its ds_read
+// (res26-narrow's 20-pixel maps at d = 1); 0: read from the arguments.
+template <int C, int MODE, int FW = 0, int FD = 0, int FTH = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
   static_assert(C <= 20, "conv3x3d_kernel: C <= 20");
   constexpr int K = 9 * C, KT = (K + 15) / 16, NG = (C + 3) / 4, PF = 8;  // PF: reads in flight
   __shared__ __attribute__((aligned(16))) float tdl[2 * TD_BUF / 4];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int d = a.g.d, W = a.W, H = a.H;
-  const TdGeo G = td_geo(C, W, a.g.TH);
+  constexpr bool FIX = FW > 0 && FD > 0 && FTH > 0;
+  const int d = FIX ? FD : a.g.d, W = FIX ? FW : a.W, H = a.H;
+  const TdGeo G = td_geo(C, W, FIX ? FTH : a.g.TH);
   float wt[NG][KT];
 #pragma unroll
   for (int g = 0; g < NG; ++g)
@@ -671,6 +675,13 @@ static int td_rows(int C, int H, int W, int d) {
   if (th < 1) return 0;
   const int nb = (hc + th - 1) / th;
   return (hc + nb - 1) / nb;
+}
+
+// the compile-time geometry instance (res26-narrow: 20-pixel maps, d = 1, 25-row tiles)
+// applies; HONK_TD_FIXED=0 turns it off (A/B)
+static bool td_fixed(const Conv3Args& a) {
+  const char* e = getenv("HONK_TD_FIXED");
+  return !(e && e[0] == '0') && a.W == 20 && a.g.d == 1 && a.g.TH == 25;
 }
 
 // class rows per conv3x3m_kernel tile: C planes of (TH + 2) x (W + 2d) (+ pad) in TM_XL
@@ -955,7 +966,8 @@ __host__ __device__ inline int twd_nchunk(int C, int W, int TH) {
   return (C * g.PS / 4 + C * twd_ds(TH, W) / 4 + 63) / 64 * 64;
 }
 
-template <int C>
+// FW, FD, FTH (all > 0): compile-time tile geometry, as conv3x3d_kernel's
+template <int C, int FW = 0, int FD = 0, int FTH = 0>
 __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   static_assert(C > 16 && C <= 20, "wgrad3x3d_kernel: 16 < C <= 20");
   constexpr int K9 = 9 * C, NJ = (K9 + 15) / 16, NH = (K9 + 63) / 64;
@@ -963,7 +975,8 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i16 = lane & 15, kk = lane >> 4;
-  const int d = a.g.d, W = a.W, H = a.H, TH = a.g.TH;
+  constexpr bool FIX = FW > 0 && FD > 0 && FTH > 0;
+  const int d = FIX ? FD : a.g.d, W = FIX ? FW : a.W, H = a.H, TH = FIX ? FTH : a.g.TH;
   const TdGeo G = td_geo(C, W, TH);
   const int DS = twd_ds(TH, W), XF = C * G.PS;  // dy planes start at float XF
   const int nch = twd_nchunk(C, W, TH);
@@ -1135,6 +1148,13 @@ static int twd_rows(int C, int H, int W, int d) {
   if (th < 1) return 0;
   const int nb = (hc + th - 1) / th;
   return (hc + nb - 1) / nb;
+}
+
+// wgrad3x3d_kernel's compile-time geometry instance (res26-narrow: W = 20, d = 1, 17-row
+// bands); HONK_TD_FIXED=0 turns it off (A/B)
+static bool twd_fixed(const WgradArgs& a) {
+  const char* e = getenv("HONK_TD_FIXED");
+  return !(e && e[0] == '0') && a.W == 20 && a.g.d == 1 && a.g.TH == 17;
 }
 
 // class rows per wgrad3x3m_kernel tile: C x planes of (TH + 2) x (W + 2d) in TW_XL,
@@ -1763,7 +1783,8 @@ extern "C" int honk_conv3x3_f32(const float* x, const float* w, float* y, int64_
   if (tdr > 0) {
     a.g = train::class_bands(h, dil, tdr);
     const int gd = (int)std::min<int64_t>((int64_t)a.B * a.g.nband, cu_count());
-    hipLaunchKernelGGL((train::conv3x3d_kernel<19, 0>), dim3(gd), dim3(512), 0, st, a);
+    if (train::td_fixed(a)) hipLaunchKernelGGL((train::conv3x3d_kernel<19, 0, 20, 1, 25>), dim3(gd), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((train::conv3x3d_kernel<19, 0>), dim3(gd), dim3(512), 0, st, a);
   } else if (c == 19 && !(ke && ke[0] == 'v') && train::tm_rows(c, h, w_, dil) > 0) {
     a.g = train::class_bands(h, dil, train::tm_rows(c, h, w_, dil));
     const int gm = train::tc_grid((int64_t)a.B * a.g.nband);
@@ -1836,7 +1857,8 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
   a.g = wp.g;
   const int grid = wp.grid;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (wp.dma) hipLaunchKernelGGL((train::wgrad3x3d_kernel<19>), dim3(grid), dim3(512), 0, st, a);
+  if (wp.dma && train::twd_fixed(a)) hipLaunchKernelGGL((train::wgrad3x3d_kernel<19, 20, 1, 17>), dim3(grid), dim3(512), 0, st, a);
+  else if (wp.dma) hipLaunchKernelGGL((train::wgrad3x3d_kernel<19>), dim3(grid), dim3(512), 0, st, a);
   else if (wp.mfma) hipLaunchKernelGGL((train::wgrad3x3m_kernel<19>), dim3(grid), dim3(256), 0, st, a);
   else if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((train::wgrad3x3_kernel<45>), dim3(grid), dim3(512), 0, st, a);
@@ -1987,8 +2009,14 @@ extern "C" int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, 
   a.mask = nullptr;
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (mode == 1) hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
-  else hipLaunchKernelGGL((train::conv3x3d_kernel<19, 2>), dim3(S), dim3(512), 0, st, a);
+  if (train::td_fixed(a)) {
+    if (mode == 1) hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1, 20, 1, 25>), dim3(S), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((train::conv3x3d_kernel<19, 2, 20, 1, 25>), dim3(S), dim3(512), 0, st, a);
+  } else if (mode == 1) {
+    hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((train::conv3x3d_kernel<19, 2>), dim3(S), dim3(512), 0, st, a);
+  }
   tl.done(st);
   HONK_LAUNCH_CHECK("conv3x3d_kernel");
   return HONK_OK;
@@ -2014,7 +2042,8 @@ extern "C" int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, u
   a.mask = mask;
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
+  if (train::td_fixed(a)) hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1, 20, 1, 25>), dim3(S), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
   tl.done(st);
   HONK_LAUNCH_CHECK("conv3x3d_kernel (tail epilogue)");
   return HONK_OK;

@@ -329,3 +329,29 @@ def test_fused_tail_step_bitwise(monkeypatch, name, n_layers, B):
         assert torch.equal(g1[k], g2[k]), k
     for k in b1:
         assert torch.equal(b1[k], b2[k]), k
+
+
+def test_fixed_geometry_instances_bitwise(monkeypatch):
+    """The compile-time res26-narrow geometry instances of conv3x3d_kernel (every MODE)
+    and wgrad3x3d_kernel vs the runtime-geometry ones (HONK_TD_FIXED=0): one training
+    step, bit-identical loss and gradients."""
+    cfg = dict(hm.find_config("res26-narrow"))
+    cfg["n_layers"] = 4
+
+    def step():
+        torch.manual_seed(7)
+        m = hm.find_model("res26-narrow")(cfg).to(DEV).train()
+        g = torch.Generator(device=DEV).manual_seed(8)
+        x = torch.randn(40, 101, 40, device=DEV, generator=g)
+        y = torch.randint(0, 12, (40,), device=DEV, generator=g)
+        loss = torch.nn.functional.cross_entropy(m(x), y)
+        loss.backward()
+        return loss.detach(), {k: p.grad.clone() for k, p in m.named_parameters()}
+
+    monkeypatch.delenv("HONK_TD_FIXED", raising=False)
+    l1, g1 = step()
+    monkeypatch.setenv("HONK_TD_FIXED", "0")
+    l2, g2 = step()
+    assert torch.equal(l1, l2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
