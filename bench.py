@@ -489,6 +489,18 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
         opt.step(grad_scale=hd.allreduce_grads(flat))
         return loss
 
+    # parity of the timed workload itself (outside the timed region): the first step's
+    # training-mode loss on the native kernels vs the same model on stock PyTorch ops
+    # (MIOpen convs, ATen BatchNorm / mean / Linear / cross-entropy), same weights and batch
+    import copy
+    with torch.no_grad():
+        m_nat, m_ref = copy.deepcopy(model), copy.deepcopy(model)
+        m_ref.honk_native_train = False
+        l_nat = float(crit(m_nat(x), y))
+        l_ref = float(torch.nn.functional.cross_entropy(m_ref(x), y))
+        del m_nat, m_ref
+    torch.cuda.empty_cache()
+
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
@@ -512,6 +524,9 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
                    "per_gpu_batch": B, "global_batch": ctx.world * B,
                    "parallelism": f"dp{ctx.world}: one flat fp32 grad bucket all-reduce ({flat.numel} params)"},
         "final_loss": float(loss.item()),
+        "parity": {"step0_loss_native": l_nat, "step0_loss_pytorch_fp32": l_ref, "abs_diff": abs(l_nat - l_ref),
+                   "note": "first step's train-mode loss, native kernels vs stock PyTorch ops on the same weights "
+                           "and 4096-clip batch (the gradients are pinned by tests/test_train_golden.py)"},
         "roofline": {"bound": "mfma", "kernel": "whole training step (per-GPU)",
                      "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),

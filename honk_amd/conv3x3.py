@@ -145,7 +145,7 @@ class _Conv3x3(torch.autograd.Function):
     """h = conv(x, w).  Statistics boxes (dicts shared with honk_amd's res tails, see
     res_tail): box_out -> this conv's epilogue also sums the next tail's forward
     statistics (of relu(h) [+ old]) into box_out["fwd"], and (FUSE_TAIL) writes the
-    tail's s = relu(h) [+ old] in place of h plus the ReLU mask (box_out["mask"]): the
+    tail's s = relu(h) [+ old] in place of h plus the ReLU bit mask (box_out["mask"]): the
     returned tensor then holds s, which only the tail reads (autograd still sees h: the
     gradient it hands back is the tail's gh); box_in (the box of the tail whose output x
     is) -> the input-gradient conv sums that tail's backward statistics (of dx and
@@ -166,7 +166,7 @@ class _Conv3x3(torch.autograd.Function):
                 if FUSE_TAIL:
                     x = x.contiguous()
                     s = torch.empty_like(x)
-                    mask = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+                    mask = torch.empty(B, H, W, dtype=torch.int32, device=x.device)  # bit o: channel o
                     _native.check(_native.load().honk_conv3x3_tail_f32(
                         x.data_ptr(), w.data_ptr(), s.data_ptr(), mask.data_ptr(), B, C, H, W, d,
                         oc.data_ptr() if oc is not None else None, buf.data_ptr(), buf.numel(),

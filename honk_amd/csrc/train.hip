@@ -124,8 +124,9 @@ struct Conv3Args {
   const float* aux;  // MODE 1: the residual old (may be null); MODE 2: the BN output y
   double* part;      // [C][gridDim.x][2] per-workgroup partial sums
   // MODE 1 only, may be null: y receives s = relu(conv) [+ aux] instead of conv, and
-  // mask[i] = !(conv <= 0) (the ReLU's backward mask, torch's threshold_backward)
-  unsigned char* mask;
+  // mask[b][p] bit o = !(conv[b][o][p] <= 0) (the ReLU's backward mask, torch's
+  // threshold_backward; one 32-bit word per pixel, C <= 20)
+  unsigned* mask;
 };
 
 typedef float tf2 __attribute__((ext_vector_type(2)));
@@ -541,6 +542,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
   float* pyb = a.y;
   size_t ppix = 0;
   bool ppv = false;  // the pending super tile has a valid pixel in this lane
+  unsigned pbits = 0u;  // MODE 1 with a mask: the pending pixel's ReLU bits so far
   auto epi = [&](int o) {
     if (o < C && ppv) {
       const float v = pacc[o >> 2][o & 3];
@@ -549,7 +551,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
         if (a.aux) sv = sv + pav[o];
         if (a.mask) {
           pyb[(size_t)o * H * W + ppix] = sv;
-          a.mask[(size_t)(pyb - a.y) + (size_t)o * H * W + ppix] = v <= 0.f ? 0 : 1;
+          pbits |= (v <= 0.f ? 0u : 1u) << o;
+          if (o == C - 1) a.mask[(size_t)(pyb - a.y) / C + ppix] = pbits;  // the pixel's word, once
         } else {
           pyb[(size_t)o * H * W + ppix] = v;
         }
@@ -626,6 +629,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
       pyb = yb;
       ppix = pix;
       ppv = pv;
+      pbits = 0u;
     }
   }
   // the last super tile's epilogue
@@ -1428,7 +1432,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const float* __restrict__
 }
 
 // g = v[c] (gy - u[c] - y w[c]) [+ gs]; gold (may be null) = g; gh = h > 0 ? g : 0
-// (MASK: the conv epilogue's byte mask !(h <= 0) in place of h)
+// (MASK: the conv epilogue's bit mask in place of h: word [b][p], bit c = !(h <= 0))
 template <bool MASK>
 __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ y,
                                                        const float* __restrict__ gs, const void* __restrict__ hm,
@@ -1437,17 +1441,19 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__
                                                        float* __restrict__ gold, int64_t total, int C, int HW) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float* h = (const float*)hm;
-  const unsigned char* mk = (const unsigned char*)hm;
+  const unsigned* mk = (const unsigned*)hm;
   if ((HW & 3) == 0) {
     const int64_t i4 = 4 * i;
     if (i4 >= total) return;
-    const int c = (int)((i4 / HW) % C);
+    const int64_t bc = i4 / HW;
+    const int c = (int)(bc % C);
     const float4 av = *(const float4*)(gy + i4), bv = *(const float4*)(y + i4);
     float4 hv;
     if constexpr (MASK) {
-      const unsigned mw = *(const unsigned*)(mk + i4);  // 4 mask bytes: 1 = h > 0 (or NaN)
-      hv = float4{(mw & 0xffu) ? 1.f : 0.f, (mw & 0xff00u) ? 1.f : 0.f, (mw & 0xff0000u) ? 1.f : 0.f,
-                  (mw & 0xff000000u) ? 1.f : 0.f};
+      // the 4 pixels' words (pixel p = i4 - bc HW of clip b = bc / C)
+      const uint4 mw = *(const uint4*)(mk + (bc / C) * HW + (i4 - bc * HW));
+      hv = float4{((mw.x >> c) & 1u) ? 1.f : 0.f, ((mw.y >> c) & 1u) ? 1.f : 0.f, ((mw.z >> c) & 1u) ? 1.f : 0.f,
+                  ((mw.w >> c) & 1u) ? 1.f : 0.f};
     } else {
       hv = *(const float4*)(h + i4);
     }
@@ -1463,11 +1469,12 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__
     return;
   }
   if (i >= total) return;
-  const int c = (int)((i / HW) % C);
+  const int64_t bc = i / HW;
+  const int c = (int)(bc % C);
   float g = v[c] * (gy[i] - u[c] - y[i] * w[c]);
   if (gs) g = g + gs[i];
   if (gold) gold[i] = g;
-  if constexpr (MASK) gh[i] = mk[i] ? g : 0.f;
+  if constexpr (MASK) gh[i] = ((mk[(bc / C) * HW + (i - bc * HW)] >> c) & 1u) ? g : 0.f;
   else gh[i] = h[i] <= 0.f ? 0.f : g;
 }
 
@@ -2022,7 +2029,7 @@ extern "C" int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, 
   return HONK_OK;
 }
 
-extern "C" int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, unsigned char* mask, int64_t batch,
+extern "C" int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, uint32_t* mask, int64_t batch,
                                      int32_t c, int32_t h, int32_t w_, int32_t dil, const float* old, void* stats,
                                      size_t stats_bytes, void* stream) {
   int rc = tc_check(x, w, s, batch, c, h, w_, dil);
@@ -2071,7 +2078,7 @@ extern "C" int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, fl
 }
 
 extern "C" int honk_res_tail_bwd_mask_f32(const float* gy, const float* gs, const float* y, const float* invstd,
-                                          const unsigned char* mask, float* gh, float* gold, int64_t batch, int32_t c,
+                                          const uint32_t* mask, float* gh, float* gold, int64_t batch, int32_t c,
                                           int32_t hh, int32_t ww, int32_t dil, void* stats, size_t stats_bytes,
                                           void* stream) {
   if (!gy || !y || !invstd || !mask || !gh || !stats) return fail(HONK_ERR_ARG, "null pointer argument");

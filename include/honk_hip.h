@@ -260,15 +260,16 @@ int honk_res_tail_bwd_f32(const float* gy, const float* gs, const float* y, cons
 /*
  * The forward conv of a res block with the tail's elementwise head in its epilogue (the
  * statistics epilogue's shapes): s = relu(conv(x, w)) [+ old] is written instead of the
- * conv output (NCHW, as x), mask[i] = !(conv <= 0) (one byte per element: the ReLU's
- * backward mask, NaN counts as > 0 as in torch's threshold_backward), and the statistics
+ * conv output (NCHW, as x), the ReLU's backward mask as one 32-bit word per pixel
+ * (mask[b][h][w] bit o = !(conv[b][o][h][w] <= 0): NaN counts as > 0, as in torch's
+ * threshold_backward; these shapes have c <= 20), and the statistics
  * of s as honk_conv3x3_stats_f32 mode 1.  Then honk_res_tail_fwd_s_f32 makes
  * y = BatchNorm_train(s) from s alone, and honk_res_tail_bwd_mask_f32 is
  * honk_res_tail_bwd_part_f32 with the mask in place of the conv output: the tails read
  * neither the conv output nor old, and write no separate s.  Same fp32 operations as the
  * unfused tails (bit-identical given the same statistics).
  */
-int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, unsigned char* mask, int64_t batch, int32_t c,
+int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, uint32_t* mask, int64_t batch, int32_t c,
                           int32_t h, int32_t w_, int32_t dil, const float* old, void* stats, size_t stats_bytes,
                           void* stream);
 int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, float* invstd, float* running_mean,
@@ -278,7 +279,7 @@ int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, float* invstd
  * dilation dil); dil = 0: `stats` is a workspace of honk_bn_train_workspace_bytes(batch, c,
  * hh * ww) and the statistics are summed here (a block whose output feeds no conv). */
 int honk_res_tail_bwd_mask_f32(const float* gy, const float* gs, const float* y, const float* invstd,
-                               const unsigned char* mask, float* gh, float* gold, int64_t batch, int32_t c,
+                               const uint32_t* mask, float* gh, float* gold, int64_t batch, int32_t c,
                                int32_t hh, int32_t ww, int32_t dil, void* stats, size_t stats_bytes, void* stream);
 size_t honk_conv3x3_stats_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil);
 int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,

@@ -74,7 +74,10 @@ def record(dec: Decisions):
         if box is not None and "mask" in box:
             # the fused tail: the conv's output holds s = relu(h) [+ old]; its epilogue
             # wrote the ReLU decision itself (!(h <= 0))
-            dec.relu.append(box["mask"].bool().cpu())
+            # one 32-bit word per pixel, bit o = channel o's decision
+            bits = box["mask"].cpu().to(torch.int64)
+            C = h.shape[1]
+            dec.relu.append(torch.stack([((bits >> o) & 1).bool() for o in range(C)], 1))
         else:
             dec.relu.append((h > 0).detach().cpu())
         return h
