@@ -475,18 +475,22 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
     model = hm.find_model(name)(cfg).to(ctx.dev).train()
     hd.broadcast_module(model)
     flat = FlatParams(model)
+    fbuf = hd.FlatBuffers(model)      # BN running stats: one broadcast per step
+    reducer = hd.GradAllReduce(flat)  # one all-reduce per step, started by backward's last gradient
     opt = FlatSGD(flat, lr=0.1, momentum=0.9, weight_decay=1e-5)
     crit = CrossEntropyLoss()
     g = torch.Generator(device=ctx.dev).manual_seed(99 + ctx.rank)
     x = torch.randn(B, 101, 40, device=ctx.dev, generator=g)
     y = torch.randint(0, cfg["n_labels"], (B,), device=ctx.dev, generator=g)
+    from honk_amd.head_train import check_labels
+    check_labels(y, cfg["n_labels"])  # once: the batch is fixed
 
     def step():
         opt.zero_grad()
-        hd.broadcast_module(model, buffers_only=True)
-        loss = crit(model(x), y)
+        hd.broadcast_buffers(fbuf)
+        loss = crit(model(x), y, labels_checked=True)
         loss.backward()
-        opt.step(grad_scale=hd.allreduce_grads(flat))
+        opt.step(grad_scale=reducer.wait())
         return loss
 
     # parity of the timed workload itself (outside the timed region): the first step's
@@ -522,7 +526,8 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
         "per_rank_clips_s": [round(B * args.steps / t, 1) for t in per],
         "config": {"workload": f"{name} training step (train-mode BN batch stats, CE loss, SGD m=0.9, wd 1e-5)",
                    "per_gpu_batch": B, "global_batch": ctx.world * B,
-                   "parallelism": f"dp{ctx.world}: one flat fp32 grad bucket all-reduce ({flat.numel} params)"},
+                   "parallelism": f"dp{ctx.world}: per step one broadcast of the BN-stat bucket and one all-reduce "
+                                  f"of the flat fp32 grad bucket ({flat.numel} params)"},
         "final_loss": float(loss.item()),
         "parity": {"step0_loss_native": l_nat, "step0_loss_pytorch_fp32": l_ref, "abs_diff": abs(l_nat - l_ref),
                    "note": "first step's train-mode loss, native kernels vs stock PyTorch ops on the same weights "

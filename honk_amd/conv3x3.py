@@ -66,21 +66,22 @@ def _same_ws(B, C, H, W, d, device):
     return torch.empty(max(n, 1), dtype=torch.uint8, device=device), n
 
 
-_warned = set()
-
-
-def warn_fallback(model, what):
-    """Say once per (model, reason) that a training step left the native kernels, so
-    a configuration outside their envelope is not silently slow."""
-    key = (id(model), what)
-    if key in _warned:
+def warn_fallback(model, what, phase="training"):
+    """Say once per (model, reason) that a forward left the native kernels, so a
+    configuration outside their envelope is not silently slow.  ``phase`` names the
+    forward that fell back ("training" or "the eval forward").  The once-only record
+    lives on the module itself (a reused id() of a collected model cannot suppress a
+    new model's warning)."""
+    seen = model.__dict__.setdefault("_honk_warned", set())
+    key = (phase, what)
+    if key in seen:
         return
-    _warned.add(key)
+    seen.add(key)
     import warnings
     if what.startswith("the eval forward"):
         msg = f"honk_amd: {type(model).__name__}: {what}"
     else:
-        msg = f"honk_amd: {type(model).__name__} training falls back to PyTorch/MIOpen for {what}"
+        msg = f"honk_amd: {type(model).__name__} {phase} falls back to PyTorch/MIOpen for {what}"
     warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
@@ -391,6 +392,11 @@ class _Stem(torch.autograd.Function):
         return None, dw, None, None
 
 
+# honk_res_stem_*: the bordered (H+2) x (W+2) map in LDS (static up to 8192 floats,
+# dynamic LDS beyond, up to the CU's 160 KiB less the reduction buffer)
+STEM_MAX_PIXELS = 160 * 256 - 256 * 9
+
+
 def stem_supported(x, conv0, pool) -> bool:
     """[B, H, W] fp32 input that needs no gradient, conv0 = Conv2d(1, C, 3, padding 1,
     no bias), AvgPool2d with stride = kernel and no padding (or no pool)."""
@@ -398,7 +404,7 @@ def stem_supported(x, conv0, pool) -> bool:
         return False
     if not (tuple(conv0.kernel_size) == (3, 3) and tuple(conv0.padding) == (1, 1) and conv0.bias is None
             and tuple(conv0.stride) == (1, 1) and tuple(conv0.dilation) == (1, 1) and conv0.in_channels == 1
-            and conv0.out_channels >= 1 and (x.shape[1] + 2) * (x.shape[2] + 2) <= 8192):
+            and conv0.out_channels >= 1 and (x.shape[1] + 2) * (x.shape[2] + 2) <= STEM_MAX_PIXELS):
         return False
     if pool is None:
         return True

@@ -43,6 +43,11 @@ inline int fail(int code, const char* fmt, ...) {
                           hipGetErrorString(_e));                                      \
   } while (0)
 
+// ReLU with torch.relu's NaN behaviour: x <= 0 (either zero included) -> +0,
+// otherwise x -- a NaN of either sign passes (v_cmp + v_cndmask; fmaxf(x, 0) and an
+// integer max on the bits would turn a NaN, resp. a -NaN, into 0)
+__device__ __forceinline__ float relu_keepnan(float x) { return x <= 0.f ? 0.f : x; }
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // number of CUs of the current device (cached per device)

@@ -59,7 +59,7 @@ __device__ __forceinline__ float row_lse(const float* z, int n, float& mx) {
 
 // loss = mean_b (lse(z_b) - z_b[y_b]); one workgroup, rows strided over its threads,
 // per-thread double sums combined by a fixed LDS tree.  A label outside [0, n) makes
-// the loss NaN (torch raises; here the caller sees the NaN).
+// the loss NaN (torch raises: head_train.py checks the labels before the launch).
 __global__ __launch_bounds__(CE_THREADS) void ce_fwd_kernel(const float* __restrict__ z,
                                                            const int64_t* __restrict__ y, float* __restrict__ loss,
                                                            int64_t batch, int n) {
@@ -82,7 +82,8 @@ __global__ __launch_bounds__(CE_THREADS) void ce_fwd_kernel(const float* __restr
 }
 
 // dz[b][j] = (softmax(z_b)[j] - [j == y_b]) * g / batch, g = *gloss (the upstream
-// gradient of the mean loss, a device scalar)
+// gradient of the mean loss, a device scalar); a row whose label is outside [0, n)
+// gets NaN, as its loss term (head_train.py checks labels before either kernel)
 __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ y,
                                                      const float* __restrict__ gloss, float* __restrict__ dz,
                                                      int64_t batch, int n) {
@@ -93,7 +94,8 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ z
   const float lse = row_lse(zb, n, mx);
   const float scale = *gloss / (float)batch;
   const int64_t t = y[b];
-  for (int j = 0; j < n; ++j) dz[b * n + j] = (expf(zb[j] - lse) - (j == t ? 1.f : 0.f)) * scale;
+  const bool ok = t >= 0 && t < n;
+  for (int j = 0; j < n; ++j) dz[b * n + j] = ok ? (expf(zb[j] - lse) - (j == t ? 1.f : 0.f)) * scale : NAN;
 }
 
 }  // namespace head

@@ -310,7 +310,7 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
         f32x4 v, o;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          v[k] = fmaxf(acc[m][k], 0.f) + rv[m][k];
+          v[k] = relu_keepnan(acc[m][k]) + rv[m][k];
           o[k] = fmaf(v[k], bsc[k], bsh[k]);
         }
         const int so = m * 16 * G::CP * 4;
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
             for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
               for (int kx = 0; kx < 3; ++kx) acc = fmaf(win[a + ky][bb + kx], wr[ky * 3 + kx], acc);
-            s += fmaxf(acc, 0.f);
+            s += relu_keepnan(acc);
           }
         v[u] = (PH * PW > 1) ? s * inv : s;
         if (ONES && c4 + u == C) v[u] = 1.f;
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(256) void conv0_generic_kernel(const float* __restr
               const float xv = (ir >= 0 && ir < Hin && ic >= 0 && ic < Win) ? xb[(int64_t)ir * Win + ic] : 0.f;
               acc = fmaf(xv, w0[c * 9 + ky * 3 + kx], acc);
             }
-          s += fmaxf(acc, 0.f);
+          s += relu_keepnan(acc);
         }
       if (PH * PW > 1) s *= inv;
     }

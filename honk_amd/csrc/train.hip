@@ -1489,7 +1489,10 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__
 // each thread accumulates its channel's 9 weight gradients, summed over the Q
 // threads of a channel in a fixed order into one partial per workgroup (wsum_kernel).
 // ---------------------------------------------------------------------------- //
-constexpr int STEM_XL = 8192;  // floats of the staged (H+2) x (W+2) map
+constexpr int STEM_XL = 8192;  // floats of the staged (H+2) x (W+2) map (static LDS kernels)
+// maps past STEM_XL (the wide eval fallback, e.g. 101 x 160 inputs): stem_kernel with the
+// image and the reduction buffer in dynamic LDS, up to the CU's 160 KiB
+constexpr int STEM_XL_DYN = 160 * 256 - 256 * 9;  // floats
 
 struct StemArgs {
   const float* x;   // [B][H][W]
@@ -1558,10 +1561,13 @@ __device__ __forceinline__ void stem_border(float* xs, int H, int W) {
   }
 }
 
-template <bool BWD>
+template <bool BWD, bool DYN = false>
 __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
-  __shared__ float xs[STEM_XL];
-  __shared__ float red[256 * 9];
+  __shared__ float xs_s[DYN ? 1 : STEM_XL];
+  __shared__ float red_s[DYN ? 1 : 256 * 9];
+  extern __shared__ float dyn_lds[];
+  float* xs = DYN ? dyn_lds + 256 * 9 : xs_s;
+  float* red = DYN ? dyn_lds : red_s;
   const int Q = 256 / a.C, o = threadIdx.x / Q, q = threadIdx.x - o * Q;
   const bool act = o < a.C;
   float wr[9], dw[9];
@@ -1697,7 +1703,13 @@ __global__ __launch_bounds__(256) void stem_tile_kernel(StemArgs a) {
 template <bool BWD>
 static void stem_launch(const StemArgs& a, int grid, hipStream_t st) {
   const int Wq = a.W / a.pw;
-  if (a.ph == 2 && a.pw == 2) hipLaunchKernelGGL((stem_tile_kernel<BWD, 2, 2, 1>), dim3(grid), dim3(256), 0, st, a);
+  const int xl = (a.H + 2) * (a.W + 2);
+  if (xl > STEM_XL) {
+    const unsigned bytes = (unsigned)(256 * 9 + xl) * 4u;
+    (void)hipFuncSetAttribute((const void*)stem_kernel<BWD, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    hipLaunchKernelGGL((stem_kernel<BWD, true>), dim3(grid), dim3(256), bytes, st, a);
+  } else if (a.ph == 2 && a.pw == 2) hipLaunchKernelGGL((stem_tile_kernel<BWD, 2, 2, 1>), dim3(grid), dim3(256), 0, st, a);
   else if (a.ph == 4 && a.pw == 3) hipLaunchKernelGGL((stem_tile_kernel<BWD, 4, 3, 1>), dim3(grid), dim3(256), 0, st, a);
   else if (a.ph == 1 && a.pw == 1 && Wq % 4 == 0)
     hipLaunchKernelGGL((stem_tile_kernel<BWD, 1, 1, 4>), dim3(grid), dim3(256), 0, st, a);
@@ -2163,7 +2175,8 @@ int stem_check(const void* x, const void* w, const void* y, int64_t batch, int32
   if (batch < 0 || batch > 0x7fffffff || h < 1 || w_ < 1 || ph < 1 || pw < 1 || ph > h || pw > w_)
     return fail(HONK_ERR_ARG, "bad stem shape (B=%lld H=%d W=%d pool %dx%d)", (long long)batch, h, w_, ph, pw);
   if (c < 1 || c > 64) return fail(HONK_ERR_UNSUPPORTED, "stem: %d feature maps (1..64)", c);
-  if ((h + 2) * (w_ + 2) > train::STEM_XL) return fail(HONK_ERR_UNSUPPORTED, "stem: %dx%d input too large", h, w_);
+  if ((int64_t)(h + 2) * (w_ + 2) > train::STEM_XL_DYN)
+    return fail(HONK_ERR_UNSUPPORTED, "stem: %dx%d input too large ((H+2)(W+2) <= %d)", h, w_, train::STEM_XL_DYN);
   return HONK_OK;
 }
 int stem_grid(int64_t batch) { return (int)std::min<int64_t>(batch, 3 * (int64_t)cu_count()); }

@@ -103,7 +103,9 @@ def world_info():
 
 
 def broadcast_module(module, src: int = 0, buffers_only: bool = False):
-    """Make every rank's parameters/buffers equal to rank `src`'s (DDP start / broadcast_buffers)."""
+    """Make every rank's parameters/buffers equal to rank `src`'s (DDP start).  One
+    collective per tensor: the training loop's per-step buffer sync uses FlatBuffers /
+    broadcast_buffers instead (one collective per step)."""
     rank, world = _ctx()
     if world == 1:
         return
@@ -123,3 +125,88 @@ def allreduce_grads(flat) -> float:
         return 1.0
     dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM)
     return 1.0 / world
+
+
+class FlatBuffers:
+    """The module's floating-point buffers (BatchNorm running_mean / running_var) re-homed
+    into ONE contiguous tensor, so DDP's broadcast_buffers is one collective per step.
+
+    Semantics (DDP with broadcast_buffers=True): before every training forward each
+    rank takes rank 0's running statistics; each rank then updates its copy from its
+    own batch statistics, and rank 0's copy is what eval / save see.  The integer
+    ``num_batches_tracked`` counters are not in the bucket: every rank increments them
+    once per forward from the same starting value (broadcast_module at start), so
+    they stay equal without a collective.  Kernels that update the statistics through
+    raw pointers (the native train-mode BatchNorm) write straight into the bucket.
+    """
+
+    def __init__(self, module: torch.nn.Module):
+        bufs = [b for b in module.buffers() if b.is_floating_point()]
+        self.buffers = bufs
+        if not bufs:
+            self.data = None
+            return
+        dtypes = {b.dtype for b in bufs}
+        devs = {b.device for b in bufs}
+        if len(dtypes) != 1 or len(devs) != 1:
+            raise ValueError(f"FlatBuffers: buffers of one dtype and device expected, got {dtypes} on {devs}")
+        n = sum(b.numel() for b in bufs)
+        self.data = torch.empty(n, dtype=bufs[0].dtype, device=bufs[0].device)
+        off = 0
+        for b in bufs:
+            k = b.numel()
+            self.data[off:off + k].copy_(b.reshape(-1))
+            b.data = self.data[off:off + k].view_as(b)
+            off += k
+
+
+def broadcast_buffers(fb: FlatBuffers, src: int = 0):
+    """ONE broadcast of the buffer bucket from rank `src` (utils/train.py:129's forward
+    under DDP's broadcast_buffers)."""
+    rank, world = _ctx()
+    if world == 1 or fb.data is None:
+        return
+    dist.broadcast(fb.data, src)
+
+
+class GradAllReduce:
+    """ONE all-reduce (sum) of the flat gradient bucket per step, started the moment
+    backward has written the bucket's last gradient (a post-accumulate-grad hook on
+    every parameter counts them; the last one launches the collective asynchronously
+    on the backend's stream), so it overlaps autograd's teardown and the host work
+    before the optimizer step.  ``wait()`` returns the 1/world scale the fused SGD
+    kernel applies (the DDP mean).  One backward per step (no gradient accumulation
+    across backward calls: a second backward would add into a bucket already on the
+    wire)."""
+
+    def __init__(self, flat):
+        self.flat = flat
+        self.world = _ctx()[1]
+        self.work = None
+        self.count = 0
+        self.handles = []
+        if self.world > 1:
+            for p in flat.params:
+                self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def _hook(self, p):
+        self.count += 1
+        if self.count == len(self.flat.params):
+            self.work = dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM, async_op=True)
+
+    def wait(self) -> float:
+        if self.world == 1:
+            return 1.0
+        if self.work is None:
+            # a parameter received no gradient this step: reduce now (same result)
+            dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
+        else:
+            self.work.wait()
+        self.work = None
+        self.count = 0
+        return 1.0 / self.world
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+        self.handles = []

@@ -133,9 +133,30 @@ class _CrossEntropy(torch.autograd.Function):
         return dz, None
 
 
-def cross_entropy(scores, labels):
-    """F.cross_entropy(scores, labels) (mean reduction) on the native kernels."""
-    if supported(scores) and scores.dim() == 2 and scores.shape[0] > 0:
+def check_labels(labels, n):
+    """torch's own check (nn.CrossEntropyLoss raises on a class index outside [0, n)):
+    on the host for CPU labels, one min/max reduction (a sync) for device labels --
+    the native kernels would only see a NaN loss.  The training loop checks the
+    loader's host labels before they go to the device (no sync on the hot path)."""
+    if labels.numel() == 0:
+        return
+    lo, hi = (int(v) for v in torch.aminmax(labels))
+    if lo < 0 or hi >= n:
+        bad = lo if lo < 0 else hi
+        raise IndexError(f"Target {bad} is out of bounds.")
+
+
+def cross_entropy(scores, labels, labels_checked=False):
+    """F.cross_entropy(scores, labels) (mean reduction) on the native kernels: float32
+    ROCm scores [B, n] with B > 0 and a [B] class-index target.  Anything else the
+    native op does not implement (probability targets, other shapes, CPU tensors)
+    takes PyTorch's op; out-of-range class indices raise as in torch
+    (``labels_checked``: the caller already ran check_labels on a host copy)."""
+    if (supported(scores) and scores.dim() == 2 and scores.shape[0] > 0 and labels.dim() == 1
+            and labels.shape[0] == scores.shape[0] and not labels.is_floating_point()
+            and not labels.is_complex() and labels.dtype != torch.bool):
+        if not labels_checked:
+            check_labels(labels, scores.shape[1])
         return _CrossEntropy.apply(scores, labels)
     return F.cross_entropy(scores, labels)
 
@@ -144,5 +165,5 @@ class CrossEntropyLoss(torch.nn.Module):
     """nn.CrossEntropyLoss() as the training loop uses it (utils/train.py:99): native
     on float32 ROCm tensors, PyTorch's op otherwise."""
 
-    def forward(self, scores, labels):
-        return cross_entropy(scores, labels)
+    def forward(self, scores, labels, labels_checked=False):
+        return cross_entropy(scores, labels, labels_checked)

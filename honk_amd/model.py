@@ -165,6 +165,7 @@ class SpeechResModel(SerializableModule):
     # and each block's relu / residual / train-mode BatchNorm on honk_res_tail_*
     # (honk_amd/conv3x3.py), the mean and the Linear on honk_amd/head_train.py
     def _torch_forward(self, x, native_convs=False):
+        phase = "training" if self.training else "the eval forward"
         x_in, x = x, x.unsqueeze(1)
         box_in = None
         for i in range(self.n_layers + 1):
@@ -175,10 +176,10 @@ class SpeechResModel(SerializableModule):
                 x = old_x = _conv3x3.stem(x_in, conv, pool)
                 continue
             if native_convs and i == 0:
-                _conv3x3.warn_fallback(self, "the stem (conv0 + relu + pool)")
+                _conv3x3.warn_fallback(self, "the stem (conv0 + relu + pool)", phase)
             if native_convs and i > 0 and not _conv3x3.supported(x, conv):
                 _conv3x3.warn_fallback(self, f"the block convs ({conv.weight.shape[0]} maps, "
-                                             f"{tuple(x.shape[2:])} map, dilation {conv.dilation[0]})")
+                                             f"{tuple(x.shape[2:])} map, dilation {conv.dilation[0]})", phase)
             if native_convs and i > 0 and _conv3x3.supported(x, conv) and \
                     _conv3x3.bn_supported(x, getattr(self, "bn{}".format(i))):
                 # conv, then relu / residual add / train BatchNorm as one fused tail
@@ -217,7 +218,7 @@ class SpeechResModel(SerializableModule):
                     x = _conv3x3.batch_norm_train(x, bn)
                 else:
                     if native_convs and bn.training:
-                        _conv3x3.warn_fallback(self, "train-mode BatchNorm")
+                        _conv3x3.warn_fallback(self, "train-mode BatchNorm", phase)
                     x = bn(x)
         if native_convs and _head.supported(x):
             return _head.linear(_head.spatial_mean(x), self.output)

@@ -138,9 +138,11 @@ def train(config, datasets=None):
     HIP kernel on ROCm).  When torch.distributed is initialised with world > 1
     this is data-parallel with DDP semantics: each rank
     draws ``batch_size`` clips per step from its shard of the train set, BN uses
-    per-replica batch statistics with running stats broadcast from rank 0, the
-    gradient bucket is summed with ONE all-reduce and averaged in the SGD kernel.
-    Only rank 0 prints and saves.
+    per-replica batch statistics with running stats broadcast from rank 0 (ONE
+    broadcast of the flat buffer bucket per step), the gradient bucket is summed
+    with ONE all-reduce -- started from the hook of the last gradient backward
+    writes -- and averaged in the SGD kernel: two collectives per step.  Only rank
+    0 prints and saves.
     """
     rank, world = hd.world_info()
     log = rank == 0
@@ -156,6 +158,8 @@ def train(config, datasets=None):
         model.cuda()
     hd.broadcast_module(model)
     flat = FlatParams(model)
+    fbuf = hd.FlatBuffers(model)     # BN running stats: one broadcast per step
+    reducer = hd.GradAllReduce(flat)  # grads: one all-reduce per step, started by backward
     optimizer = _sgd(flat, config, config["lr"][0])
     schedule_steps = config["schedule"]  # the caller's list, extended in place (utils/train.py:100-101)
     schedule_steps.append(np.inf)
@@ -183,13 +187,15 @@ def train(config, datasets=None):
         for model_in, labels in train_loader:
             model.train()
             optimizer.zero_grad()
+            labels_host = labels
             if not config["no_cuda"]:
                 model_in, labels = model_in.cuda(), labels.cuda()
-            hd.broadcast_module(model, buffers_only=True)
+            hd.broadcast_buffers(fbuf)
             scores = model(model_in)
-            loss = criterion(scores, labels)
+            head_train.check_labels(labels_host, scores.shape[1])  # torch's IndexError, on the host copy
+            loss = criterion(scores, labels, labels_checked=True)
             loss.backward()
-            optimizer.step(grad_scale=hd.allreduce_grads(flat))
+            optimizer.step(grad_scale=reducer.wait())
             step_no += 1
             if step_no > schedule_steps[sched_idx]:
                 sched_idx += 1

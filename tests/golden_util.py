@@ -25,7 +25,7 @@ def ref_configs():
 
 def fixture_names():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith(("evaluate_", "train_", "caller_", "augment")))
+                  if not os.path.basename(p).startswith(("evaluate_", "train_", "caller_", "augment", "nonfinite_")))
 
 
 def load_fixture(name):

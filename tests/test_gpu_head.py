@@ -90,7 +90,21 @@ def test_cross_entropy(B, N, scale):
     assert torch.equal(loss, ht.CrossEntropyLoss()(zd, y.to(DEV)))
 
 
-def test_cross_entropy_bad_label_is_nan():
-    z = torch.randn(4, 5, device=DEV)
+def test_cross_entropy_bad_label_raises_and_kernels_agree():
+    """A class index outside [0, n) raises as torch does (checked before the native op);
+    the kernels themselves give NaN for the bad row in the loss AND its gradient row."""
+    z = torch.randn(4, 5, device=DEV, requires_grad=True)
+    for bad in (7, 5, -1):
+        y = torch.tensor([0, 1, bad, 2], device=DEV)
+        with pytest.raises(IndexError):
+            ht.cross_entropy(z, y)
+        with pytest.raises(IndexError):
+            torch.nn.CrossEntropyLoss()(z.detach().cpu(), y.cpu())
     y = torch.tensor([0, 1, 7, 2], device=DEV)
-    assert torch.isnan(ht.cross_entropy(z, y))
+    loss = ht._CrossEntropy.apply(z, y)
+    assert torch.isnan(loss)
+    (gz,) = torch.autograd.grad(loss, z)
+    assert torch.isnan(gz[2]).all()
+    # probability targets / other shapes take PyTorch's op
+    p = torch.softmax(torch.randn(4, 5, device=DEV), 1)
+    assert torch.allclose(ht.cross_entropy(z, p), torch.nn.functional.cross_entropy(z, p))

@@ -61,3 +61,18 @@ def test_train_on_gpu_then_native_eval(tmp_path, capsys):
         cpu = m(xs[:8]).numpy()
         gpu = m.to(DEV)(xs[:8].to(DEV)).cpu().numpy()
     np.testing.assert_allclose(gpu, cpu, atol=1e-4, rtol=0)
+
+
+def test_train_bad_label_raises(tmp_path):
+    """A label outside [0, n_labels) stops train() with torch's IndexError (the native
+    cross-entropy would otherwise return a NaN loss and keep stepping)."""
+    cfg = dict(hm.find_config("res8-narrow"))
+    cfg.update(ht.default_run_config(str(tmp_path / "m.pt")))
+    cfg.update(no_cuda=False, gpu_no=0, n_epochs=1, dev_every=1, batch_size=8, lr=[0.05], schedule=[])
+    cfg["model_class"] = hm.find_model("res8-narrow")
+    xs = torch.randn(16, 101, 40)
+    ys = torch.randint(0, 12, (16,))
+    ys[3] = 12
+    ds = torch.utils.data.TensorDataset(xs, ys)
+    with pytest.raises(IndexError):
+        ht.train(cfg, datasets=(ds, ds, ds))

@@ -238,7 +238,10 @@ def test_res_tail_bitwise_vs_unfused(B, C, H, W, res, keep):
 
 
 @pytest.mark.parametrize("B,C,H,W,pool", [(64, 19, 101, 40, (2, 2)), (5, 45, 101, 40, (4, 3)),
-                                          (3, 19, 101, 40, None), (2, 45, 101, 40, None), (3, 19, 9, 7, (2, 3))])
+                                          (3, 19, 101, 40, None), (2, 45, 101, 40, None), (3, 19, 9, 7, (2, 3)),
+                                          # past the static LDS image (dynamic LDS): wide eval inputs
+                                          (2, 45, 101, 160, None), (3, 19, 101, 160, (2, 2)),
+                                          (2, 8, 180, 200, (4, 3))])
 def test_res_stem_matches_float64(B, C, H, W, pool):
     """honk_res_stem_fwd_f32 / wgrad_f32 (conv0 + relu [+ AvgPool2d], model.py:104-110)
     vs the same ops in float64 on the CPU: output within 1e-6 and the conv0 weight

@@ -103,3 +103,105 @@ def test_dp_step_equals_mean_of_shard_grads():
     flat.grad.copy_(torch.from_numpy(mean))
     FlatSGD(flat, lr=0.05, momentum=0.9, weight_decay=1e-5).step()
     np.testing.assert_allclose(res[0][1], flat.data.numpy(), rtol=1e-6, atol=1e-7)
+
+
+def _count_worker(rank, world, port, tmp, out):
+    """train() on 2 gloo ranks (CPU), every torch.distributed collective counted."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from honk_amd import train as htr
+    calls = []
+    for fn in ("broadcast", "all_reduce", "all_gather", "reduce_scatter", "barrier", "all_to_all"):
+        orig = getattr(dist, fn)
+
+        def wrap(*a, _orig=orig, _fn=fn, **k):
+            calls.append(_fn)
+            return _orig(*a, **k)
+        setattr(dist, fn, wrap)
+    name = "res8-narrow"
+    cfg = dict(hm.find_config(name))
+    cfg.update(htr.default_run_config(os.path.join(tmp, f"m{rank}.pt")))
+    cfg.update(no_cuda=True, n_epochs=2, dev_every=1, batch_size=4, lr=[0.05], schedule=[])
+    cfg["model_class"] = hm.find_model(name)
+    # a starting checkpoint (train() loads it; evaluate() falls back to it when no dev
+    # accuracy beats 0 -- the reference's best_model = None quirk)
+    init = os.path.join(tmp, f"init{rank}.pt")
+    torch.manual_seed(0)
+    hm.find_model(name)(cfg).save(init)
+    cfg["input_file"] = init
+    g = torch.Generator().manual_seed(3)
+    ds = torch.utils.data.TensorDataset(torch.randn(16, 101, 40, generator=g), torch.randint(0, 12, (16,), generator=g))
+    torch.manual_seed(rank)
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        htr.train(cfg, datasets=(ds, ds, ds))
+    m = hm.find_model(name)(cfg)
+    n_init = len(list(m.parameters())) + len(list(m.buffers()))   # broadcast_module at start
+    out[rank] = (calls, n_init)
+    dist.destroy_process_group()
+
+
+def test_train_two_collectives_per_step(tmp_path):
+    """DP train(): after the start-up broadcast of the module, exactly ONE broadcast (the
+    BN running-stat bucket) and ONE all-reduce (the gradient bucket) per step."""
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_count_worker, args=(2, port, str(tmp_path), out), nprocs=2, join=True)
+        res = dict(out)
+    steps = 2 * (16 // 2 // 4)   # 2 epochs x (8 clips per rank / batch 4)
+    for r in (0, 1):
+        calls, n_init = res[r]
+        assert calls[:n_init] == ["broadcast"] * n_init
+        loop = calls[n_init:]
+        assert loop == ["broadcast", "all_reduce"] * steps, loop
+
+
+def _hook_worker(rank, world, port, out):
+    """GradAllReduce (hook-started async all-reduce) == the synchronous all-reduce."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = []
+    for use_hook in (False, True):
+        m = _model(seed=0)
+        flat = FlatParams(m)
+        fb = hd.FlatBuffers(m)
+        red = hd.GradAllReduce(flat) if use_hook else None
+        x, y = _batch(8)
+        s, e = hd.shard_bounds(8, rank, world)
+        m.train()
+        flat.zero_grad()
+        hd.broadcast_buffers(fb)
+        torch.nn.CrossEntropyLoss()(m(x[s:e]), y[s:e]).backward()
+        scale = red.wait() if use_hook else hd.allreduce_grads(flat)
+        res.append((flat.grad.clone().numpy() * scale, fb.data.clone().numpy()))
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_grad_hook_allreduce_equals_sync():
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_hook_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    for r in (0, 1):
+        (g_sync, b_sync), (g_hook, b_hook) = res[r]
+        np.testing.assert_array_equal(g_sync, g_hook)
+        np.testing.assert_array_equal(b_sync, b_hook)
+    np.testing.assert_array_equal(res[0][1][0], res[1][1][0])
+
+
+def test_flat_buffers_rehome_keeps_state_dict():
+    m = _model(seed=2)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    fb = hd.FlatBuffers(m)
+    assert fb.data.numel() == sum(b.numel() for b in m.buffers() if b.is_floating_point())
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+    # a train-mode forward updates the running stats inside the bucket
+    before = fb.data.clone()
+    m.train()(torch.randn(3, 101, 40))
+    assert not torch.equal(before, fb.data)
+    assert m.bn1.running_mean.data_ptr() == fb.data.data_ptr()

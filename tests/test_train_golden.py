@@ -70,15 +70,17 @@ def _dp_worker(rank, world, port, name, out):
                 p.add_(1.0)
     hd.broadcast_module(m)
     flat = FlatParams(m)
+    fbuf = hd.FlatBuffers(m)
+    reducer = hd.GradAllReduce(flat)
     opt = FlatSGD(flat, lr=float(z["lr"]), momentum=float(z["momentum"]), weight_decay=float(z["weight_decay"]),
                   nesterov=bool(z["nesterov"]))
     s, e = hd.shard_bounds(z["x"].shape[0], rank, world)
     m.train()
     opt.zero_grad()
-    hd.broadcast_module(m, buffers_only=True)
+    hd.broadcast_buffers(fbuf)
     loss = torch.nn.CrossEntropyLoss()(m(torch.from_numpy(z["x"][s:e])), torch.from_numpy(z["y"][s:e]))
     loss.backward()
-    scale = hd.allreduce_grads(flat)
+    scale = reducer.wait()
     g = {k: (p.grad * scale).numpy().copy() for k, p in m.named_parameters()}
     opt.step(grad_scale=scale)
     out[rank] = (float(loss.item()), g, {k: p.detach().numpy().copy() for k, p in m.named_parameters()},
@@ -219,15 +221,31 @@ def _dp_gpu_worker(rank, world, port, name, out):
     hd.broadcast_module(m)
     state = {k: v.detach().clone() for k, v in m.state_dict().items()}
     flat = FlatParams(m)
+    fbuf = hd.FlatBuffers(m)
     opt = FlatSGD(flat, **_opt_args(z))
     xn, yn = tg.inputs(z)
     s, e = hd.shard_bounds(xn.shape[0], rank, world)
     opt.zero_grad()
-    hd.broadcast_module(m, buffers_only=True)
-    dec, loss = _record_step(m, torch.from_numpy(xn[s:e]).to("cuda:0"), torch.from_numpy(yn[s:e]).to("cuda:0"))
-    loss.backward()
+    hd.broadcast_buffers(fbuf)
+    # the local gradient, before the reduction: this rank's backward without the hook
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)   # a fallback warning fails the worker
+        dec, loss = _record_step(m, torch.from_numpy(xn[s:e]).to("cuda:0"), torch.from_numpy(yn[s:e]).to("cuda:0"))
+        loss.backward()
     local = {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}
-    scale = hd.allreduce_grads(flat)
+    # the train() machinery: the same step again, the all-reduce started by backward's hook
+    reducer = hd.GradAllReduce(flat)
+    opt.zero_grad()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        m.load_state_dict(state)
+        hd.broadcast_buffers(fbuf)
+        loss2 = torch.nn.CrossEntropyLoss()(m(torch.from_numpy(xn[s:e]).to("cuda:0")),
+                                            torch.from_numpy(yn[s:e]).to("cuda:0"))
+        loss2.backward()
+    assert float(loss2.item()) == float(loss.item())
+    scale = reducer.wait()
     opt.step(grad_scale=scale)
     r = dr.replay_step(cfg, str(z["model"]), state, xn[s:e], yn[s:e], dec, _opt_args(z))
     gerr = max(dr.rel_err(local[k], r["g"][k]) for k in local)
