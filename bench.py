@@ -34,7 +34,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense pe
 HBM_PEAK_GBS = 8000.0
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 # MFMA peak per precision mode in ALGORITHMIC flop: bf16x3 spends 3 bf16 products per MAC
-MODE_PEAK = {"f32": FP32_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3, "bf16": BF16_MFMA_PEAK_TFLOPS}
+# (f16x2: fp16 MFMA, same dense peak as bf16, 2 products per MAC)
+MODE_PEAK = {"f32": FP32_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3, "bf16": BF16_MFMA_PEAK_TFLOPS,
+             "f16x2": BF16_MFMA_PEAK_TFLOPS / 2}
 WORKLOADS = {
     "res15": "res15 eval forward (SpeechResModel, 13 dilated 3x3 res layers, 45 maps, 12 labels)",
     "res8": "res8 eval forward (SpeechResModel, avg-pool 4x3, 6 res layers, 45 maps, 12 labels)",
@@ -46,6 +48,10 @@ PREC_NOTES = {
     "f32": "IEEE fp32 on v_mfma_f32_16x16x4_f32; 1e-4 logit parity",
     "bf16": "bf16 activations/weights, fp32 accumulation; top-1 parity only (reduced precision vs the fp32 "
             "reference), so never the headline",
+    "f16x2": "activations as fp16 (RNE), weights (input BN folded) as fp16 (hi, lo), products w_hi*x + w_lo*x on "
+             "fp16 MFMA, fp32 accumulation; meets the fp32 1e-4 logit parity bar on res15 (goldens and calibrated "
+             "random cases, tests/test_gpu_f16x2.py; simulated worst 3.8e-5, exp/f16_mix_sim.py); pooled res8/res26 "
+             "maps 5e-4",
 }
 
 
@@ -59,7 +65,7 @@ def parse(argv=None):
     p.add_argument("--model", default="res15")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--precision", default="bf16x3", choices=["bf16x3", "f32", "bf16"],
+    p.add_argument("--precision", default="bf16x3", choices=["bf16x3", "f32", "bf16", "f16x2"],
                    help="res path arithmetic: bf16x3 (fp32 values as bf16 hi/lo pairs, 3 bf16 MFMA products, "
                         "fp32 accumulation; 1e-4 parity), f32 (fp32 MFMA; 1e-4 parity) or bf16 (top-1 parity)")
     p.add_argument("--no-alt", action="store_true",
@@ -304,6 +310,7 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
         kname = "honk::res::block_kernel (dilated 3x3 conv, fp32 MFMA)"
     else:
         sp = 2 if prec == "bf16x3" else 1
+        tag = "f16" if prec == "f16x2" else f"sp{sp}"
         act = H * W * CP * 2 * sp
         per_clip, layer = 0, 1
         for k in plan:
@@ -314,13 +321,14 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
                 per_clip += act * (1 + (1 if layer % 2 == 0 else 0) + (1 if layer < L else 0))
                 layer += 1
         dom = max(set(plan), key=plan.count)
-        traffic = load_traffic(f"{dom}_sp{sp}", clips, model)
+        traffic = load_traffic(f"{dom}_{tag}", clips, model)
         what = {"block16p_kernel": "fused odd + even layer pair", "block16w_kernel": "weight-stationary layer",
                 "block16l_kernel": "last layer on the pair's streaming machinery, fused channel sums",
                 "block16r_kernel": "row-band layer"}
-        kname = (" + ".join(f"honk::res::{k}<..., SP={sp}> x{plan.count(k)} ({what[k]})"
+        kname = (" + ".join(f"honk::res::{k}<..., {tag}> x{plan.count(k)} ({what[k]})"
                             for k in sorted(set(plan), key=plan.index))
-                 + f" per chunk: dilated 3x3 convs, bf16 MFMA{', 3 products' if sp == 2 else ''}")
+                 + " per chunk: dilated 3x3 convs, "
+                 + {"bf16x3": "bf16 MFMA, 3 products", "bf16": "bf16 MFMA", "f16x2": "fp16 MFMA, 2 products"}[prec])
     secs = kms * 1e-3
     bw = per_clip * clips * chunk_fwds / secs / 1e9 if nl and secs else None
     out = {"bound": "mfma", "kernel": kname,
@@ -336,7 +344,7 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
                    "achieved_GBs": round(bw, 1) if bw else None, "peak_GBs": HBM_PEAK_GBS,
                    "frac": round(bw / HBM_PEAK_GBS, 4) if bw else None}}
     del out["avg_ms_per_launch"]
-    if prec == "bf16x3" and ach:
+    if prec in ("bf16x3", "f16x2") and ach:
         out["frac_of_raw_bf16_peak"] = round(ach / BF16_MFMA_PEAK_TFLOPS, 4)
     return out
 
@@ -617,7 +625,7 @@ def rank_main(args):
     alts = {}
     if not args.no_alt and not args.e2e:
         if is_res:
-            for other in ("f32", "bf16"):
+            for other in ("bf16x3", "f16x2", "f32", "bf16"):
                 if other != prec:
                     log(f"res {other} mode")
                     alts[f"{other}_mode"] = measure_res(ctx, args, args.model, other, B, x=x, model=model)

@@ -22,7 +22,7 @@ class ResDesc(ctypes.Structure):
         "n_labels", "n_maps", "n_layers", "use_dilation", "pool_h", "pool_w", "height", "width", "precision")]
 
 
-PRECISIONS = {"f32": 0, "bf16": 1, "bf16x3": 2}
+PRECISIONS = {"f32": 0, "bf16": 1, "bf16x3": 2, "f16x2": 3}
 
 
 class CnnDesc(ctypes.Structure):

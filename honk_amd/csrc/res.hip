@@ -348,6 +348,11 @@ __device__ __forceinline__ void store4(__bf16* o, f32x4 v) {
   const b4 b = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
   *(b4*)o = b;
 }
+__device__ __forceinline__ void store4(_Float16* o, f32x4 v) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 b = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+  *(h4*)o = b;
+}
 
 // Thread = output pixel (weights wave-uniform: scalar loads); the block's 256
 // pixels x CP channels are staged in LDS and written back as one contiguous
@@ -580,8 +585,13 @@ struct Layout {
   int C, CP, NT, L, NL, prec;
   int Hin, Win, H, W, ph, pw;
   size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, off_frag16, frag16_floats,
-      off_fragx3, fragx3_floats, off_bias16, total;
+      off_fragx3, fragx3_floats, off_fragh, off_bias16, total;
 };
+
+// operand format of the bf16-pipe kernels (res_bf16w.inc): 0 bf16, 1 bf16x3, 2 f16x2;
+// activation parts in memory (2 for bf16x3 only)
+static int fmt_of(int prec) { return prec == HONK_PREC_BF16X3 ? 1 : prec == HONK_PREC_F16X2 ? 2 : 0; }
+static int sp_of(int fm) { return fm == 1 ? 2 : 1; }
 
 static size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
 
@@ -592,7 +602,7 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
                 d->n_maps, d->n_layers, d->n_labels, d->height, d->width);
   if (d->n_maps > 64 || (d->n_maps > 48 && d->precision != HONK_PREC_F32))
     return fail(HONK_ERR_UNSUPPORTED,
-                "n_feature_maps=%d: the gfx950 kernels take up to 64 maps in precision f32, 48 in bf16 / bf16x3",
+                "n_feature_maps=%d: the gfx950 kernels take up to 64 maps in precision f32, 48 in bf16 / bf16x3 / f16x2",
                 d->n_maps);
   L->C = d->n_maps;
   L->NT = (d->n_maps + 15) / 16;
@@ -621,11 +631,14 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   L->frag16_floats = (size_t)g16_frag_bytes(L->NT, 1) / 4;
   L->off_fragx3 = L->off_frag16 + L->frag16_floats * L->L;
   L->fragx3_floats = (size_t)g16_frag_bytes(L->NT, 2) / 4;
+  // fp16 (hi, lo) weight fragments for HONK_PREC_F16X2 (same layout and size as bf16x3's)
+  L->off_fragh = L->off_fragx3 + L->fragx3_floats * L->L;
   // folded input-BN bias [L][16 classes][CP] for the bf16 kernel
-  L->off_bias16 = L->off_fragx3 + L->fragx3_floats * L->L;
+  L->off_bias16 = L->off_fragh + L->fragx3_floats * L->L;
   L->total = L->off_bias16 + (size_t)16 * L->CP * L->L;
   L->prec = d->precision;
-  if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16 && L->prec != HONK_PREC_BF16X3)
+  if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16 && L->prec != HONK_PREC_BF16X3 &&
+      L->prec != HONK_PREC_F16X2)
     return fail(HONK_ERR_ARG, "unknown precision %d", d->precision);
   return HONK_OK;
 }
@@ -699,7 +712,8 @@ static int max_bands_per_clip(const Layout& L, int TH, int use_dilation) {
 // slowest wave's m-tiles x the MFMA cycles of one m-tile plus a fixed per-tile
 // cost (barrier, first operand reads) -- among the heights whose (TH + 2)-row
 // image (W + d pixels per row + 1) fits the staging buffer.  0: does not fit.
-static int plan_w_th(const Layout& L, int SP, int d) {
+static int plan_w_th(const Layout& L, int FM, int d) {
+  const int SP = sp_of(FM);
   const int imgpx = g16w_img_px(L.NT, SP);
   const int RW = L.W + d;
   int thmax = (imgpx - 1) / RW - 2;
@@ -715,7 +729,7 @@ static int plan_w_th(const Layout& L, int SP, int d) {
   while (thmax >= 1 && ((long)(thmax + 1) * d * RB + RB) / 16 >= 0xffff) --thmax;
   if (thmax < 1) return 0;
   const int ksa = (18 * L.NT + 3) / 4;
-  const double c_mt = ksa * L.NT * (SP == 2 ? 3 : 1) * 16.0, c_tile = 1500.0;
+  const double c_mt = ksa * L.NT * (FM == 1 ? 3 : FM == 2 ? 2 : 1) * 16.0, c_tile = 1500.0;
   int best = 0;
   double best_cost = 1e300;
   for (int th = thmax; th >= 1; --th) {
@@ -738,9 +752,9 @@ static int plan_w_th(const Layout& L, int SP, int d) {
 }
 static int dil_of(const honk_res_desc* d, int i) { return d->use_dilation ? (1 << ((i - 1) / 3)) : 1; }
 // bands per clip of layer i under the weight-stationary plan (0: a layer does not fit)
-static int bands_w(const Layout& L, const honk_res_desc* d, int SP, int i) {
+static int bands_w(const Layout& L, const honk_res_desc* d, int FM, int i) {
   const int dl = dil_of(d, i);
-  const int th = plan_w_th(L, SP, dl);
+  const int th = plan_w_th(L, FM, dl);
   return th ? band_geo(L.H, dl, th).nbc : 0;
 }
 // Which bf16 / bf16x3 block kernel runs: the weight-stationary one where it was
@@ -752,14 +766,15 @@ struct PairPlan {
   int lag, NRA, NRB, slotb, ppr, ppw;  // ppw: DMA pieces per A wave per step
   int ns;                              // streams per workgroup (block16p_kernel NS)
 };
-static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t n, int grid, int i);
-static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
+static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i);
+static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
   // 45-map bf16x3: the weight-stationary path (with fused pairs); bf16: only when
   // pairs fuse (the single weight-stationary layer is slower than the row-band one)
-  // (measured: res15 bf16 +4 %; res8's 13-pixel rows lose 20 % -- row-band there)
-  bool want = L.NT == 3 && (SP == 2 || (L.W >= 32 && L.L >= 3 && pair_at(L, d, SP, 4096, 256, 1).ok));
+  // (measured: res15 bf16 +4 %; res8's 13-pixel rows lose 20 % -- row-band there);
+  // f16x2: always (its only kernels)
+  bool want = FM == 2 || (L.NT == 3 && (FM == 1 || (L.W >= 32 && L.L >= 3 && pair_at(L, d, FM, 4096, 256, 1).ok)));
   if (const char* e = getenv("HONK_RES_KERNEL")) {
-    if (e[0] == 'r') return false;
+    if (e[0] == 'r' && FM != 2) return false;
     if (e[0] == 'w') want = true;
   }
   if (!want) return false;
@@ -767,7 +782,7 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int SP) {
   if (L.C >= L.CP) return false;  // no zero-padding channel for the folded bias
   if (L.ph * L.pw > 1 && !((L.ph == 2 && L.pw == 2) || (L.ph == 4 && L.pw == 3))) return false;  // conv0 shapes
   for (int i = 1; i <= L.L; ++i)
-    if (!bands_w(L, d, SP, i)) return false;
+    if (!bands_w(L, d, FM, i)) return false;
   return true;
 }
 
@@ -852,8 +867,9 @@ static int pair_ppw(int SP, int ppr) {
   if (SP == 2) return ppr == 9 ? 9 : ppr == 5 ? 10 : ppr == 3 ? 9 : 0;
   return ppr == 4 ? 4 : ppr == 2 ? 5 : 0;
 }
-static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t n, int grid, int i) {
+static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i) {
   const PairPlan no{false, 0, 0, 0, 0, 0, 0, 1};
+  const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
   if (i % 2 == 0 || i + 1 >= L.L) return no;
@@ -863,7 +879,7 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t
   if (!sB || cb >= 0xE0000000ull) return no;
   // bf16 with full 40-pixel rows: two streams per workgroup when both rings fit half the LDS
   const char* nse = getenv("HONK_PAIR_STREAMS");
-  if (SP == 1 && !(nse && nse[0] == '1')) {
+  if (FM == 0 && !(nse && nse[0] == '1')) {
     const PairPlan p2 = plan_pair(L, SP, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2);
     if (p2.ok && p2.ppr == 4 && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
   }
@@ -878,8 +894,9 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int SP, int64_t
 // stream's share of the LDS.  One clip per stream pass: the plan of a 1-clip stream
 // (no A-out ring: NRB = 1 unused slot, no lag).  HONK_LAST_KERNEL=w keeps the
 // weight-stationary kernel (the pair-vs-w bitwise tests).
-static PairPlan last_at(const Layout& L, const honk_res_desc* d, int SP, int i) {
+static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) {
   const PairPlan no{false, 0, 0, 0, 0, 0, 0, 1};
+  const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   const char* lenv = getenv("HONK_LAST_KERNEL");
   if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r')) || (lenv && lenv[0] == 'w')) return no;
@@ -896,30 +913,28 @@ static PairPlan last_at(const Layout& L, const honk_res_desc* d, int SP, int i) 
   return pp.ok ? pp : no;
 }
 
-template <int NT, int SP>
+template <int NT, int FM>
 static int launch_block16w(const Block16WArgs& a, hipStream_t st) {
+  constexpr int SP = FM == 1 ? 2 : 1;
   int grid = cu_count();
   if (grid > a.ntiles) grid = a.ntiles;
-  const dim3 gd(grid), bd(G16W<NT, SP>::NTHREADS);
+  const dim3 gd(grid), bd(G16W<NT, SP, FM>::NTHREADS);
   const bool last = a.chsum != nullptr, res = a.res != nullptr;
-  if (last && res) hipLaunchKernelGGL((block16w_kernel<NT, SP, true, true>), gd, bd, 0, st, a);
-  else if (last) hipLaunchKernelGGL((block16w_kernel<NT, SP, true, false>), gd, bd, 0, st, a);
-  else if (res) hipLaunchKernelGGL((block16w_kernel<NT, SP, false, true>), gd, bd, 0, st, a);
-  else hipLaunchKernelGGL((block16w_kernel<NT, SP, false, false>), gd, bd, 0, st, a);
+  if (last && res) hipLaunchKernelGGL((block16w_kernel<NT, SP, true, true, FM>), gd, bd, 0, st, a);
+  else if (last) hipLaunchKernelGGL((block16w_kernel<NT, SP, true, false, FM>), gd, bd, 0, st, a);
+  else if (res) hipLaunchKernelGGL((block16w_kernel<NT, SP, false, true, FM>), gd, bd, 0, st, a);
+  else hipLaunchKernelGGL((block16w_kernel<NT, SP, false, false, FM>), gd, bd, 0, st, a);
   HONK_LAUNCH_CHECK("res block16w_kernel");
   return HONK_OK;
 }
-static int dispatch_block16w(int NT, int SP, const Block16WArgs& a, hipStream_t st) {
-  if (SP == 1) {
-    if (NT == 1) return launch_block16w<1, 1>(a, st);
-    if (NT == 2) return launch_block16w<2, 1>(a, st);
-    if (NT == 3) return launch_block16w<3, 1>(a, st);
-  } else {
-    if (NT == 1) return launch_block16w<1, 2>(a, st);
-    if (NT == 2) return launch_block16w<2, 2>(a, st);
-    if (NT == 3) return launch_block16w<3, 2>(a, st);
-  }
-  return fail(HONK_ERR_UNSUPPORTED, "no weight-stationary kernel for NT=%d SP=%d", NT, SP);
+static int dispatch_block16w(int NT, int FM, const Block16WArgs& a, hipStream_t st) {
+#define HONK_W(nt, fm) \
+  if (NT == nt && FM == fm) return launch_block16w<nt, fm>(a, st);
+  HONK_W(1, 0) HONK_W(2, 0) HONK_W(3, 0)
+  HONK_W(1, 1) HONK_W(2, 1) HONK_W(3, 1)
+  HONK_W(1, 2) HONK_W(2, 2) HONK_W(3, 2)
+#undef HONK_W
+  return fail(HONK_ERR_UNSUPPORTED, "no weight-stationary kernel for NT=%d format %d", NT, FM);
 }
 
 template <int NT, int MT, int SP>
@@ -1006,8 +1021,12 @@ static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w
 // buffer X suffice; each layer writes exactly one tensor.
 static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* packed, const float* x,
                         float* logits, int64_t batch, int64_t chunk, void* workspace, hipStream_t st) {
-  const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;  // bf16 elements per channel value
+  const int FM = fmt_of(L.prec);  // operand format (res_bf16w.inc)
+  const int SP = sp_of(FM);       // 16-bit elements per channel value
   const size_t act = (size_t)chunk * L.H * L.W * L.CP * SP;
+  // this format's packed weight fragments (per layer)
+  const float* frb = FM == 1 ? packed + L.off_fragx3 : FM == 2 ? packed + L.off_fragh : packed + L.off_frag16;
+  const size_t frl = FM == 0 ? L.frag16_floats : L.fragx3_floats;
   __bf16* R = (__bf16*)workspace;
   __bf16* X = R + act;
   float* chsum = (float*)(R + 2 * act);
@@ -1018,30 +1037,35 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
     return fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
                 "(use precision f32)", L.W);
   int rc;
-  if (use_w_kernel(L, d, SP)) {
+  const bool wpath = use_w_kernel(L, d, FM);
+  if (!wpath && FM == 2)
+    return fail(HONK_ERR_UNSUPPORTED, "f16x2 runs on the weight-stationary / pair kernels only: %d maps, %dx%d "
+                "(pooled) map, pool %dx%d is outside their envelope (use precision f32 or bf16x3)", L.C, L.H, L.W,
+                L.ph, L.pw);
+  if (wpath) {
     // weight-stationary kernel: tiles = (clip, dilation class, band of TH class rows), TH per dilation
     int parts_last = 0;  // channel-sum partials per clip of the last layer
     for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
       const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
-      rc = (SP == 2) ? launch_conv0<__bf16, true, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
-                     : launch_conv0<__bf16, false, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+      rc = (FM == 1) ? launch_conv0<__bf16, true, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+           : (FM == 2) ? launch_conv0<_Float16, false, true>(L, x + c0 * L.Hin * L.Win, (_Float16*)R,
+                                                           packed + L.off_conv0, n, st)
+                       : launch_conv0<__bf16, false, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
       if (rc) return rc;
       int grid = cu_count();
       if (grid > n) grid = (int)n;
       for (int i = 1; i <= L.L; ++i) {
         const bool even = (i % 2) == 0;
         {
-          const PairPlan pp = pair_at(L, d, SP, n, grid, i);
+          const PairPlan pp = pair_at(L, d, FM, n, grid, i);
           if (pp.ok) {
             const int dA = dil_of(d, i);
             const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
             Block16PArgs pa;
             pa.R = R;
             pa.chsum = nullptr;
-            const float* fr = SP == 2 ? packed + L.off_fragx3 : packed + L.off_frag16;
-            const size_t fl = SP == 2 ? L.fragx3_floats : L.frag16_floats;
-            pa.wA = (const char*)(fr + (size_t)(i - 1) * fl);
-            pa.wB = (const char*)(fr + (size_t)i * fl);
+            pa.wA = (const char*)(frb + (size_t)(i - 1) * frl);
+            pa.wB = (const char*)(frb + (size_t)i * frl);
             pa.chunk_bytes = (unsigned)cb;
             pa.nclips = (int)n;
             pa.H = L.H;
@@ -1057,9 +1081,11 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.ppr = pp.ppr;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(256 * pp.ns);
-            if (SP == 2 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9, 1>), gd, bd, 0, st, pa);
-            else if (SP == 2 && pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10, 1>), gd, bd, 0, st, pa);
-            else if (SP == 2) hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9, 1>), gd, bd, 0, st, pa);
+            if (FM == 1 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9, 1>), gd, bd, 0, st, pa);
+            else if (FM == 1 && pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10, 1>), gd, bd, 0, st, pa);
+            else if (FM == 1) hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9, 1>), gd, bd, 0, st, pa);
+            else if (FM == 2 && pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1, 2>), gd, bd, 0, st, pa);
+            else if (FM == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 1, 2>), gd, bd, 0, st, pa);
             else if (pp.ppr == 4 && pp.ns == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
             else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1>), gd, bd, 0, st, pa);
             else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 1>), gd, bd, 0, st, pa);
@@ -1068,13 +1094,11 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             ++i;  // layer i + 1 done too
             continue;
           }
-          const PairPlan lp = last_at(L, d, SP, i);
+          const PairPlan lp = last_at(L, d, FM, i);
           if (lp.ok) {
             Block16PArgs pa;
             pa.R = R;  // the last (odd) layer reads R
-            const float* fr = SP == 2 ? packed + L.off_fragx3 : packed + L.off_frag16;
-            const size_t fl = SP == 2 ? L.fragx3_floats : L.frag16_floats;
-            pa.wA = pa.wB = (const char*)(fr + (size_t)(i - 1) * fl);
+            pa.wA = pa.wB = (const char*)(frb + (size_t)(i - 1) * frl);
             pa.chunk_bytes = (unsigned)((size_t)n * L.H * L.W * L.CP * 2 * SP);
             pa.nclips = (int)n;
             pa.H = L.H;
@@ -1091,7 +1115,8 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.chsum = chsum;
             TimedLaunch tl(st, layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(128 * lp.ns);
-            if (SP == 2) hipLaunchKernelGGL((block16l_kernel<3, 2, 9, 9, 2>), gd, bd, 0, st, pa);
+            if (FM == 1) hipLaunchKernelGGL((block16l_kernel<3, 2, 9, 9, 2>), gd, bd, 0, st, pa);
+            else if (FM == 2) hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2, 2>), gd, bd, 0, st, pa);
             else hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
             HONK_LAUNCH_CHECK("res block16l_kernel");
             tl.done(st);
@@ -1103,13 +1128,12 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         a.in = even ? X : R;
         a.res = even ? R : nullptr;
         a.out = (i == L.L) ? nullptr : (even ? R : X);
-        a.wfrag = (const char*)(SP == 2 ? packed + L.off_fragx3 + (size_t)(i - 1) * L.fragx3_floats
-                                        : packed + L.off_frag16 + (size_t)(i - 1) * L.frag16_floats);
+        a.wfrag = (const char*)(frb + (size_t)(i - 1) * frl);
         a.chsum = (i == L.L) ? chsum : nullptr;
         a.H = L.H;
         a.W = L.W;
         a.dil = dil_of(d, i);
-        a.TH = plan_w_th(L, SP, a.dil);
+        a.TH = plan_w_th(L, FM, a.dil);
         const BandGeo bg = band_geo(L.H, a.dil, a.TH);
         a.nbc = bg.nbc;
         a.rem = bg.rem;
@@ -1121,7 +1145,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         a.ntiles = (int)(n * a.nbc);
         if (i == L.L) parts_last = a.nbc * 4;
         TimedLaunch tl(st, layer_flop_per_clip * (double)n);
-        rc = dispatch_block16w(L.NT, SP, a, st);
+        rc = dispatch_block16w(L.NT, FM, a, st);
         tl.done(st);
         if (rc) return rc;
       }
@@ -1209,17 +1233,18 @@ int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, i
     for (int i = 1; i <= L.L; ++i) put(HONK_KERNEL_BLOCK_F32);
     return cnt;
   }
-  const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;
+  const int FM = fmt_of(L.prec), SP = sp_of(FM);
   if (plan_block16r(L, SP).TH == 0) return fail(HONK_ERR_UNSUPPORTED, "width beyond the row-band staging plan");
-  if (!use_w_kernel(L, d, SP)) {
+  if (!use_w_kernel(L, d, FM)) {
+    if (FM == 2) return fail(HONK_ERR_UNSUPPORTED, "f16x2: outside the weight-stationary / pair kernels' envelope");
     for (int i = 1; i <= L.L; ++i) put(HONK_KERNEL_ROWBAND);
     return cnt;
   }
   for (int i = 1; i <= L.L; ++i) {
-    if (pair_at(L, d, SP, n, grid, i).ok) {
+    if (pair_at(L, d, FM, n, grid, i).ok) {
       put(HONK_KERNEL_PAIR);
       ++i;
-    } else if (last_at(L, d, SP, i).ok) {
+    } else if (last_at(L, d, FM, i).ok) {
       put(HONK_KERNEL_LAST);
     } else {
       put(HONK_KERNEL_WSTAT);
@@ -1233,17 +1258,23 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   if (make_layout(d, &L) != HONK_OK || batch < 1) return 0;
   const int64_t ch = chunk_clips(L, batch);
   if (L.prec != HONK_PREC_F32) {
-    const int SP = (L.prec == HONK_PREC_BF16X3) ? 2 : 1;
+    const int FM = fmt_of(L.prec), SP = sp_of(FM);
     const PlanR pr = plan_block16r(L, SP);
     if (pr.TH == 0) {
       fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
            "(use precision f32)", L.W);
       return 0;
     }
+    const bool wpath = L.L > 0 && use_w_kernel(L, d, FM);
+    if (FM == 2 && !wpath) {
+      fail(HONK_ERR_UNSUPPORTED, "f16x2 runs on the weight-stationary / pair kernels only: %d maps, %dx%d (pooled) "
+           "map, pool %dx%d is outside their envelope (use precision f32 or bf16x3)", L.C, L.H, L.W, L.ph, L.pw);
+      return 0;
+    }
     const int nb = max_bands_per_clip(L, pr.TH, d->use_dilation);
     size_t parts = (size_t)nb * 8 * pr.MT;  // row-band kernel: [tile][wave][m-tile] channel sums
-    if (L.L > 0 && use_w_kernel(L, d, SP)) {
-      const size_t pw = (size_t)bands_w(L, d, SP, L.L) * 4;  // weight-stationary: [tile][wave]
+    if (wpath) {
+      const size_t pw = (size_t)bands_w(L, d, FM, L.L) * 4;  // weight-stationary: [tile][wave]
       if (pw > parts) parts = pw;
     }
     return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * parts * L.CP * sizeof(float);
@@ -1279,9 +1310,11 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
     const float* in_shift = in_bn ? in_bn + L.CP : nullptr;
     const int odd = ((i + 1) & 1);  // layer i + 1 (1-based) is odd
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn, in_shift, odd,
-                       (__bf16*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, 1);
+                       (unsigned short*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, 1, 0);
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn, in_shift, odd,
-                       (__bf16*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, 2);
+                       (unsigned short*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, 2, 0);
+    hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn, in_shift, odd,
+                       (unsigned short*)(packed + L.off_fragh + (size_t)i * L.fragx3_floats), L.C, L.NT, 2, 1);
     HONK_LAUNCH_CHECK("pack_block16");
     hipLaunchKernelGGL(pack_bias16_kernel, dim3(cdiv(16 * L.CP, 256)), dim3(256), 0, st, t[1 + i],
                        in_bn ? in_bn + L.CP : nullptr, packed + L.off_bias16 + (size_t)16 * L.CP * i, L.C, L.CP);

@@ -8,7 +8,10 @@ eval mode.
 
 Differences, both additive: ``evaluate``/``train`` accept injected loaders /
 datasets (the reference builds them from ``SpeechDataset.splits``, which needs
-the Speech Commands folders and librosa -- out of scope).
+the Speech Commands folders and librosa -- out of scope); a
+``honk_amd.data.DeviceSpeechDataset`` is consumed on the device (its batches are
+clip indices: ``load_audio``'s augmentation and ``collate_fn``'s MFCCs run as
+kernels, honk_amd/data.py).
 """
 from __future__ import annotations
 
@@ -25,6 +28,7 @@ import torch.utils.data as data
 
 from . import distributed as hd
 from . import head_train
+from .data import batch_input
 from . import model as mod
 from .optim import FlatParams, FlatSGD
 
@@ -104,6 +108,7 @@ def evaluate(config, model=None, test_loader=None):
     weighted, total = [], 0
     with torch.no_grad():
         for model_in, labels in test_loader:
+            model_in = batch_input(test_loader.dataset, model_in)  # device datasets: indices -> MFCCs
             if not config["no_cuda"]:
                 model_in, labels = model_in.cuda(), labels.cuda()
             scores = model(model_in)
@@ -188,6 +193,8 @@ def train(config, datasets=None):
             model.train()
             optimizer.zero_grad()
             labels_host = labels
+            # a DeviceSpeechDataset batch is clip indices: augmentation + MFCC on the device
+            model_in = batch_input(train_set, model_in)
             if not config["no_cuda"]:
                 model_in, labels = model_in.cuda(), labels.cuda()
             hd.broadcast_buffers(fbuf)
@@ -210,6 +217,7 @@ def train(config, datasets=None):
             accs = []
             with torch.no_grad():
                 for model_in, labels in dev_loader:
+                    model_in = batch_input(dev_set, model_in)
                     if not config["no_cuda"]:
                         model_in, labels = model_in.cuda(), labels.cuda()
                     scores = model(model_in)

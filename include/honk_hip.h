@@ -64,6 +64,13 @@ typedef struct honk_res_desc {
 #define HONK_PREC_F32 0
 #define HONK_PREC_BF16 1
 #define HONK_PREC_BF16X3 2
+/* fp16 activations (RNE), weights (input BN folded) as fp16 hi + lo, products
+   w_hi*x + w_lo*x on fp16 MFMA, fp32 accumulate: ~11-bit activations.  Runs on the
+   weight-stationary / pair kernels only (n_maps <= 48 with a zero-padding channel,
+   (pooled) width < 64; HONK_ERR_UNSUPPORTED otherwise).  Logit error: within the
+   1e-4 bar on res15 (simulated <= 3.8e-5, measured on the goldens); up to ~2e-4 on
+   the pooled res8 / res26 maps, which average over fewer pixels. */
+#define HONK_PREC_F16X2 3
 
 /* number of floats of the packed (kernel-layout) weight buffer */
 size_t honk_res_packed_floats(const honk_res_desc* d);
