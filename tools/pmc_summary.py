@@ -33,8 +33,11 @@ def per_kernel(path, counter):
 
 
 # kernel families: a family pools every template instance of the named kernels
-# (weighted by launches); the bf16 res kernels are split by SP (sp1 = bf16, sp2 = bf16x3)
+# (weighted by launches); the bf16-pipe res kernels are split by format (sp1 = bf16,
+# sp2 = bf16x3, f16 = f16x2)
 SP_ARG = {"block16r_kernel": 2, "block16w_kernel": 1, "block16p_kernel": 1, "block16l_kernel": 1}
+# the operand-format template argument (2 = f16x2 -> family suffix "f16")
+FM_ARG = {"block16w_kernel": 4, "block16p_kernel": 5, "block16l_kernel": 5}
 POOLS = {"block_kernel": ("block_kernel",), "conv_gemm_kernel": ("conv_gemm_kernel",),
          "c2_f32_convs": ("conv1f_kernel", "conv2f_kernel"),
          "c2_bf16x3_convs": ("conv1x3_kernel", "conv2x3_kernel"),
@@ -46,7 +49,12 @@ def families(k):
     out = []
     for fam, arg in SP_ARG.items():
         if f"::{fam}<" in k:
-            out.append(f"{fam}_sp" + k.split("<")[1].split(",")[arg].strip())
+            args = [a.strip() for a in k.split("<")[1].split(">")[0].split(",")]
+            fm = FM_ARG.get(fam)
+            if fm is not None and len(args) > fm and args[fm] == "2":
+                out.append(f"{fam}_f16")
+            else:
+                out.append(f"{fam}_sp" + args[arg])
     for fam, names in POOLS.items():
         if any(f"::{n}<" in k or f"::{n}(" in k for n in names):
             out.append(fam)
