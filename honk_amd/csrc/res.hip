@@ -532,6 +532,161 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 #include "res_bf16p.inc"
 
 // --------------------------------------------------------------------------- //
+// conv0 on the matrix cores (the bf16 / bf16x3 / f16x2 paths): 1 -> CP 3x3 pad 1,
+// ReLU, avg-pool PH x PW (model.py:87-89, 107-110), written in the block
+// kernels' activation format.  One workgroup per clip (4 waves).
+//
+// The 9-tap contraction is one v_mfma_f32_16x16x32_bf16 per (16 conv pixels,
+// 16 out channels) carrying ALL THREE bf16x3 products in its K = 32:
+//   k  0.. 8: w_hi[t] * x_hi[t]      k  9..17: w_hi[t] * x_lo[t]
+//   k 18..26: w_lo[t] * x_hi[t]      k 27..31: 0
+// (fp32 values as bf16 (hi, lo) pairs, the w_lo * x_lo term dropped: ~2^-17
+// relative, as the bf16x3 layers).  The clip's input is staged once into LDS as
+// bf16 hi and lo planes with a zero border (the conv's zero padding); a lane's B
+// fragment (its pixel, k-chunk 8g..8g+7) is 8 u16 reads at per-lane constant
+// offsets.  The weights (A: rows = out channels in the co16 order, so a lane's
+// results are aligned channel runs of its pixel) stay in registers.
+// Pooling: an m-tile = 16 pooled outputs x ONE member k of their PH x PW window;
+// the members are summed (after ReLU, row-major, as avg_pool2d) in the lanes'
+// accumulators, then divided by PH * PW.  ONES: channel C = 1.0 (the folded-bias
+// channel of the weight-stationary / pair kernels).  FM: 0 bf16, 1 bf16x3
+// ([hi CP][lo CP]), 2 fp16 output.
+// --------------------------------------------------------------------------- //
+template <int NT, int PH, int PW, int FM, bool ONES>
+__global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
+                                                     const float* __restrict__ w0, int Hin, int Win, int H, int W,
+                                                     int C) {
+  constexpr int CP = 16 * NT, P = PH * PW, SP = FM == 1 ? 2 : 1, CB = CP * 2 * SP;
+  extern __shared__ __attribute__((aligned(16))) unsigned short c0lds[];  // hi plane, lo plane
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int clip = blockIdx.x;
+  const int Wb = Win + 2, plane = (Hin + 2) * Wb;
+  unsigned short* hp = c0lds;
+  unsigned short* lp = c0lds + plane;
+
+  // weights: A fragment of n-tile n = lane (row rho = i16, k-chunk g)
+  u32x4 wa[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int co = co16(NT, n, i16);
+    unsigned short v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * g + j;
+      const int t = k < 9 ? k : k < 18 ? k - 9 : k < 27 ? k - 18 : 0;
+      // (w0 = the packed conv0 weights, [CP][9], zero rows past C: unconditional loads)
+      const float wl = w0[co * 9 + t];
+      const float w = k < 27 ? wl : 0.f;
+      const __bf16 wh = (__bf16)w;
+      const __bf16 wv = k < 18 ? wh : (__bf16)(w - (float)wh);
+      v[j] = __builtin_bit_cast(unsigned short, wv);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wa[n][j] = (unsigned)v[2 * j] | ((unsigned)v[2 * j + 1] << 16);
+  }
+  // the lane's 8 B-operand offsets (u16 elements, relative to its window's top-left
+  // in the bordered plane): slot j of chunk g = plane hi/lo, tap t.  The padding
+  // slots k >= 27 (zero weights) read the window's centre: 0 x a finite value is 0,
+  // and no per-lane select or branch guards the reads
+  int boff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * g + j;
+    const int t = k < 9 ? k : k < 18 ? k - 9 : k < 27 ? k - 18 : 4;
+    const bool lo = k >= 9 && k < 18;
+    boff[j] = (lo ? plane : 0) + (t / 3) * Wb + (t % 3);
+  }
+
+  // stage the clip: zero both planes (the border = the conv's zero padding), then the
+  // interior as bf16 (hi, lo); rows of whole float4s when W % 4 == 0
+  const float* xc = x + (size_t)clip * Hin * Win;
+  {
+    const int n16 = (2 * plane * 2 + 15) / 16;
+    for (int i = threadIdx.x; i < n16; i += 256) ((u32x4*)c0lds)[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+  auto put = [&](int r, int c, float v) {  // input (r, c) -> bordered (r + 1, c + 1)
+    const int i = (r + 1) * Wb + c + 1;
+    const __bf16 h = (__bf16)v;
+    hp[i] = __builtin_bit_cast(unsigned short, h);
+    lp[i] = __builtin_bit_cast(unsigned short, (__bf16)(v - (float)h));
+  };
+  if ((Win & 3) == 0) {
+    const int w4 = Win >> 2, n4 = Hin * w4;
+    for (int i = threadIdx.x; i < n4; i += 256) {
+      const int r = i / w4, c = (i - r * w4) * 4;
+      const f32x4 v = *(const f32x4*)(xc + (size_t)r * Win + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) put(r, c + u, v[u]);
+    }
+  } else {
+    for (int i = threadIdx.x; i < Hin * Win; i += 256) {
+      const int r = i / Win;
+      put(r, i - r * Win, xc[i]);
+    }
+  }
+  __syncthreads();
+
+  const int npo = H * W;                 // pooled outputs
+  const int ngroups = (npo + 15) >> 4;
+  char* oc = (char*)out + (size_t)clip * npo * CB;
+  for (int gi = wave; gi < ngroups; gi += 4) {
+    const int q0 = 16 * gi + i16;
+    const int q = q0 < npo ? q0 : npo - 1;
+    const int ph = q / W, pw = q - ph * W;
+    f32x4 pacc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) pacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // (two pool members per loop trip: their operand reads overlap the other's MFMAs
+    // without holding all P members' operands live)
+#pragma unroll 2
+    for (int k = 0; k < P; ++k) {
+      const int h = ph * PH + k / PW, w = pw * PW + k % PW;  // conv pixel; window top-left (h, w) bordered
+      const int base = h * Wb + w;
+      unsigned short bv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bv[j] = c0lds[base + boff[j]];
+      u32x4 b;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = (unsigned)bv[2 * j] | ((unsigned)bv[2 * j + 1] << 16);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[n]),
+                                                                  __builtin_bit_cast(bf16x8, b),
+                                                                  f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pacc[n][r] += relu_keepnan(acc[r]);
+      }
+    }
+    if (q0 >= npo) continue;
+    char* op = oc + (size_t)q0 * CB;
+    typedef typename ActT<FM == 2 ? 2 : 0>::T AT;
+    typedef typename ActT<FM == 2 ? 2 : 0>::V4 AT4;
+    AT4 hv[NT], lv[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = P > 1 ? pacc[n][r] / (float)P : pacc[n][r];
+        if (ONES && co16(NT, n, 4 * g + r) == C) v = 1.f;
+        hv[n][r] = (AT)v;
+        if constexpr (SP == 2) lv[n][r] = (AT)(v - (float)hv[n][r]);
+      }
+#pragma unroll
+    for (int pt = 0; pt < SP; ++pt) {
+      AT4* vv = pt ? lv : hv;
+#pragma unroll
+      for (int pr = 0; pr < NT / 2; ++pr) {
+        const u32x2 a0 = __builtin_bit_cast(u32x2, vv[2 * pr]), a1 = __builtin_bit_cast(u32x2, vv[2 * pr + 1]);
+        *(u32x4*)(op + pt * CP * 2 + 64 * pr + 16 * g) = u32x4{a0[0], a0[1], a1[0], a1[1]};
+      }
+      if constexpr (NT & 1) *(u32x2*)(op + pt * CP * 2 + 64 * (NT / 2) + 8 * g) = __builtin_bit_cast(u32x2, vv[NT - 1]);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- //
 // weight packing
 // --------------------------------------------------------------------------- //
 __global__ void pack_conv0_kernel(const float* __restrict__ w, float* __restrict__ out, int C, int CP) {
@@ -1015,6 +1170,43 @@ static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w
   return HONK_OK;
 }
 
+// conv0 of the bf16-pipe formats: the MFMA kernel (conv0m_kernel) where it is
+// instantiated (NT <= 3; pools 1x1, 2x2, 4x3; the staged clip within the LDS),
+// else the VALU kernel.  HONK_CONV0=v forces the VALU kernel (A/B experiments).
+template <int NT, int FM, bool ONES>
+static int launch_conv0m_nt(const Layout& L, const float* x, void* out, const float* w0, int64_t n,
+                            hipStream_t st) {
+  const unsigned lds = 2u * (unsigned)((L.Hin + 2) * (L.Win + 2)) * 2u;
+#define HONK_C0M(ph_, pw_)                                                                              \
+  if (L.ph == ph_ && L.pw == pw_) {                                                                     \
+    if (lds > 65536)                                                                                    \
+      (void)hipFuncSetAttribute((const void*)conv0m_kernel<NT, ph_, pw_, FM, ONES>,                    \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
+    hipLaunchKernelGGL((conv0m_kernel<NT, ph_, pw_, FM, ONES>), dim3((unsigned)n), dim3(256), lds, st, x, \
+                       (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C);                                  \
+    HONK_LAUNCH_CHECK("res conv0m_kernel");                                                             \
+    return HONK_OK;                                                                                     \
+  }
+  HONK_C0M(1, 1) HONK_C0M(2, 2) HONK_C0M(4, 3)
+#undef HONK_C0M
+  return 1;  // no instance
+}
+template <int FM, bool ONES>
+static int launch_conv0_16(const Layout& L, const float* x, void* out, const float* w0, int64_t n, hipStream_t st) {
+  const char* e = getenv("HONK_CONV0");
+  const bool valu = e && e[0] == 'v';
+  const bool fits = 2L * (L.Hin + 2) * (L.Win + 2) * 2 <= 160 * 1024 && n <= 0x7fffffff;
+  if (!valu && fits) {
+    int rc = 1;
+    if (L.NT == 1) rc = launch_conv0m_nt<1, FM, ONES>(L, x, out, w0, n, st);
+    else if (L.NT == 2) rc = launch_conv0m_nt<2, FM, ONES>(L, x, out, w0, n, st);
+    else if (L.NT == 3) rc = launch_conv0m_nt<3, FM, ONES>(L, x, out, w0, n, st);
+    if (rc <= 0) return rc;
+  }
+  if constexpr (FM == 2) return launch_conv0<_Float16, false, ONES>(L, x, (_Float16*)out, w0, n, st);
+  else return launch_conv0<__bf16, FM == 1, ONES>(L, x, (__bf16*)out, w0, n, st);
+}
+
 // bf16 driver: same schedule as the fp32 one (R / X0 / X1 buffers, fused mean)
 // bf16 schedule: activations stay pre-BN (see res_bf16.inc), so one residual
 // stream R (conv0 output, then every even layer's sum, in place) and one odd-layer
@@ -1047,10 +1239,9 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
     int parts_last = 0;  // channel-sum partials per clip of the last layer
     for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
       const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
-      rc = (FM == 1) ? launch_conv0<__bf16, true, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
-           : (FM == 2) ? launch_conv0<_Float16, false, true>(L, x + c0 * L.Hin * L.Win, (_Float16*)R,
-                                                           packed + L.off_conv0, n, st)
-                       : launch_conv0<__bf16, false, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+      rc = (FM == 1) ? launch_conv0_16<1, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+           : (FM == 2) ? launch_conv0_16<2, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+                       : launch_conv0_16<0, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
       if (rc) return rc;
       int grid = cu_count();
       if (grid > n) grid = (int)n;
@@ -1162,8 +1353,8 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
     int nbc_last = 0;
     for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
       const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
-      rc = (SP == 2) ? launch_conv0<__bf16, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
-                     : launch_conv0<__bf16, false>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+      rc = (SP == 2) ? launch_conv0_16<1, false>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+                     : launch_conv0_16<0, false>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
       if (rc) return rc;
       for (int i = 1; i <= L.L; ++i) {
         const bool even = (i % 2) == 0;

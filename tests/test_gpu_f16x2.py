@@ -138,7 +138,9 @@ def test_f16x2_shapes_on_weight_stationary(name, override):
     cfg.update(override)
     params, x = _res_case(cfg, 3, seed=17)
     out = run(module(cfg, params, name), x)
-    np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=POOLED_ATOL, rtol=0)
+    # one feature map: the rounding noise is not averaged over channels either
+    tol = 2 * POOLED_ATOL if cfg["n_feature_maps"] == 1 else POOLED_ATOL
+    np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=tol, rtol=0)
 
 
 def test_f16x2_batch_invariance(monkeypatch):

@@ -190,3 +190,23 @@ def test_last_kernel_batch_invariance(monkeypatch, prec):
     assert np.array_equal(full[5:9], _run(m, x[5:9]))
     monkeypatch.setenv("HONK_RES_CHUNK", "300")
     assert np.array_equal(full, _run(m, x))
+
+
+# conv0 on the matrix cores (conv0m_kernel: the three bf16x3 products in one K = 32
+# MFMA, pool members summed in the accumulators) vs the VALU conv0 (HONK_CONV0=v):
+# the same forward within the mode's bar, both against the oracle
+@pytest.mark.parametrize("prec", ["bf16x3", "f16x2", "bf16"])
+@pytest.mark.parametrize("name", ["res15", "res8", "res26", "res8-narrow", "res26-narrow", "res15-narrow"])
+def test_conv0_mfma_vs_valu(monkeypatch, name, prec):
+    cfg = dict(ref_configs()[name])
+    params, x = _case(cfg, 5, seed=43)
+    m = _module(cfg, params, name, prec)
+    ref = orc.forward(params, cfg, x)
+    outm = _run(m, x)
+    monkeypatch.setenv("HONK_CONV0", "v")
+    outv = _run(m, x)
+    bar = {"bf16x3": 1e-4, "f16x2": 5e-4, "bf16": 0.05}[prec]
+    if prec == "f16x2" and name == "res15":
+        bar = 1e-4
+    assert np.abs(outm - ref).max() <= bar and np.abs(outv - ref).max() <= bar
+    assert np.abs(outm - outv).max() <= (2e-5 if prec == "bf16x3" else bar)
