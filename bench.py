@@ -505,15 +505,19 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
 
     # parity of the timed workload itself (outside the timed region): the first step's
     # training-mode loss on the native kernels vs the same model on stock PyTorch ops
-    # (MIOpen convs, ATen BatchNorm / mean / Linear / cross-entropy), same weights and batch
+    # (MIOpen convs, ATen BatchNorm / mean / Linear / cross-entropy), same weights and batch.
+    # HONK_BENCH_TRAIN_PARITY=0 skips it (the PMC passes of tools/profile_configs.sh: only
+    # the step's own kernels in the counters)
     import copy
-    with torch.no_grad():
-        m_nat, m_ref = copy.deepcopy(model), copy.deepcopy(model)
-        m_ref.honk_native_train = False
-        l_nat = float(crit(m_nat(x), y))
-        l_ref = float(torch.nn.functional.cross_entropy(m_ref(x), y))
-        del m_nat, m_ref
-    torch.cuda.empty_cache()
+    l_nat = l_ref = None
+    if os.environ.get("HONK_BENCH_TRAIN_PARITY", "1") != "0":
+        with torch.no_grad():
+            m_nat, m_ref = copy.deepcopy(model), copy.deepcopy(model)
+            m_ref.honk_native_train = False
+            l_nat = float(crit(m_nat(x), y))
+            l_ref = float(torch.nn.functional.cross_entropy(m_ref(x), y))
+            del m_nat, m_ref
+        torch.cuda.empty_cache()
 
     for _ in range(max(1, args.warmup)):
         step()
@@ -539,7 +543,8 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
                    "parallelism": f"dp{ctx.world}: per step one broadcast of the BN-stat bucket and one all-reduce "
                                   f"of the flat fp32 grad bucket ({flat.numel} params)"},
         "final_loss": float(loss.item()),
-        "parity": {"step0_loss_native": l_nat, "step0_loss_pytorch_fp32": l_ref, "abs_diff": abs(l_nat - l_ref),
+        "parity": {"step0_loss_native": l_nat, "step0_loss_pytorch_fp32": l_ref,
+                   "abs_diff": abs(l_nat - l_ref) if l_nat is not None else None,
                    "note": "first step's train-mode loss, native kernels vs stock PyTorch ops on the same weights "
                            "and 4096-clip batch (the gradients are pinned by tests/test_train_golden.py)"},
         "roofline": {"bound": "mfma", "kernel": "whole training step (per-GPU)",
