@@ -48,6 +48,18 @@ inline int fail(int code, const char* fmt, ...) {
 // integer max on the bits would turn a NaN, resp. a -NaN, into 0)
 __device__ __forceinline__ float relu_keepnan(float x) { return x <= 0.f ? 0.f : x; }
 
+// sum over the 16 lanes of a row (lane group) by DPP: quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror -- after each step the lanes of the combined span hold
+// the same value (IEEE addition is commutative), so every lane of the row returns the
+// row's sum; VALU only (a __shfl_xor tree goes through the LDS crossbar)
+__device__ __forceinline__ float sum16_dpp(float t) {
+  t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0xB1, 0xF, 0xF, false));
+  t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0x4E, 0xF, 0xF, false));
+  t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0x141, 0xF, 0xF, false));
+  t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0x140, 0xF, 0xF, false));
+  return t;
+}
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // number of CUs of the current device (cached per device)

@@ -324,12 +324,7 @@ __global__ __launch_bounds__((Geo<NT, MT>::NTHREADS), NT) void block_kernel(Bloc
         // reduce over the 16 lanes (pixels) holding the same 4 channels
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          float t = csum[k];
-          t += __shfl_xor(t, 1);
-          t += __shfl_xor(t, 2);
-          t += __shfl_xor(t, 4);
-          t += __shfl_xor(t, 8);
-          csum[k] = t;
+          csum[k] = sum16_dpp(csum[k]);
         }
         if (i16 == 0) *(f32x4*)(a.chsum + ((size_t)tile * MW + mg) * G::CP + c4) = csum;
       }
@@ -552,7 +547,9 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 // channel of the weight-stationary / pair kernels).  FM: 0 bf16, 1 bf16x3
 // ([hi CP][lo CP]), 2 fp16 output.
 // --------------------------------------------------------------------------- //
-template <int NT, int PH, int PW, int FM, bool ONES>
+// FWB > 0: the bordered plane width Win + 2 at compile time (40-wide inputs: 42), so a
+// pool member's tap reads take their offset as an immediate
+template <int NT, int PH, int PW, int FM, bool ONES, int FWB = 0>
 __global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
                                                      const float* __restrict__ w0, int Hin, int Win, int H, int W,
                                                      int C) {
@@ -561,7 +558,7 @@ __global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, i16 = lane & 15;
   const int clip = blockIdx.x;
-  const int Wb = Win + 2, plane = (Hin + 2) * Wb;
+  const int Wb = FWB > 0 ? FWB : Win + 2, plane = (Hin + 2) * Wb;
   unsigned short* hp = c0lds;
   unsigned short* lp = c0lds + plane;
 
@@ -638,15 +635,19 @@ __global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x
     f32x4 pacc[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) pacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // (two pool members per loop trip: their operand reads overlap the other's MFMAs
-    // without holding all P members' operands live)
-#pragma unroll 2
-    for (int k = 0; k < P; ++k) {
-      const int h = ph * PH + k / PW, w = pw * PW + k % PW;  // conv pixel; window top-left (h, w) bordered
-      const int base = h * Wb + w;
+    // the lane's 8 read addresses for member 0 (window top-left (ph PH, pw PW), bordered)
+    const char* la[8];
+    {
+      const int base0 = ph * PH * Wb + pw * PW;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) la[j] = (const char*)c0lds + 2 * (base0 + boff[j]);
+    }
+    auto member = [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const int moff = 2 * ((k / PW) * Wb + k % PW);  // an immediate when FWB > 0
       unsigned short bv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bv[j] = c0lds[base + boff[j]];
+      for (int j = 0; j < 8; ++j) bv[j] = *(const unsigned short*)(la[j] + moff);
       u32x4 b;
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = (unsigned)bv[2 * j] | ((unsigned)bv[2 * j + 1] << 16);
@@ -658,7 +659,16 @@ __global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x
 #pragma unroll
         for (int r = 0; r < 4; ++r) pacc[n][r] += relu_keepnan(acc[r]);
       }
-    }
+      // (two members between fences: one's reads overlap the other's MFMAs without every
+      // member's results live at once -- the empty asm makes the sums materialise here,
+      // which a sched_barrier alone does not: the IR moves the arithmetic across it)
+      if constexpr (k & 1) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) asm volatile("" : "+v"(pacc[n]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    static_for<P>(member);
     if (q0 >= npo) continue;
     char* op = oc + (size_t)q0 * CB;
     typedef typename ActT<FM == 2 ? 2 : 0>::T AT;
@@ -668,7 +678,13 @@ __global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x
     for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = P > 1 ? pacc[n][r] / (float)P : pacc[n][r];
+        // avg_pool2d's sum / count: the reciprocal product with one FMA correction
+        float v = pacc[n][r];
+        if constexpr (P > 1) {
+          constexpr float rp = 1.0f / (float)P;
+          const float q = v * rp;
+          v = fmaf(fmaf(-q, (float)P, v), rp, q);
+        }
         if (ONES && co16(NT, n, 4 * g + r) == C) v = 1.f;
         hv[n][r] = (AT)v;
         if constexpr (SP == 2) lv[n][r] = (AT)(v - (float)hv[n][r]);
@@ -1182,8 +1198,12 @@ static int launch_conv0m_nt(const Layout& L, const float* x, void* out, const fl
     if (lds > 65536)                                                                                    \
       (void)hipFuncSetAttribute((const void*)conv0m_kernel<NT, ph_, pw_, FM, ONES>,                    \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
-    hipLaunchKernelGGL((conv0m_kernel<NT, ph_, pw_, FM, ONES>), dim3((unsigned)n), dim3(256), lds, st, x, \
-                       (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C);                                  \
+    if (L.Win == 40)                                                                                    \
+      hipLaunchKernelGGL((conv0m_kernel<NT, ph_, pw_, FM, ONES, 42>), dim3((unsigned)n), dim3(256), lds, st, x, \
+                         (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C);                                \
+    else                                                                                                \
+      hipLaunchKernelGGL((conv0m_kernel<NT, ph_, pw_, FM, ONES>), dim3((unsigned)n), dim3(256), lds, st, x, \
+                         (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C);                                \
     HONK_LAUNCH_CHECK("res conv0m_kernel");                                                             \
     return HONK_OK;                                                                                     \
   }
@@ -1385,7 +1405,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       }
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
-                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * 8 * pr.MT, L.H * L.W, L.C, L.CP, L.NL,
+                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * 8, L.H * L.W, L.C, L.CP, L.NL,
                          bn_last, bn_last + L.CP);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16 row-band)");
     }
@@ -1463,7 +1483,7 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
       return 0;
     }
     const int nb = max_bands_per_clip(L, pr.TH, d->use_dilation);
-    size_t parts = (size_t)nb * 8 * pr.MT;  // row-band kernel: [tile][wave][m-tile] channel sums
+    size_t parts = (size_t)nb * 8;  // row-band kernel: [tile][wave] channel sums
     if (wpath) {
       const size_t pw = (size_t)bands_w(L, d, FM, L.L) * 4;  // weight-stationary: [tile][wave]
       if (pw > parts) parts = pw;
