@@ -10,6 +10,7 @@ roundings, per layer:
            f16) while the residual add uses hi + lo (the stream keeps ~22 bits)
   * "f16s": as f16c, but the stored value is x - mean_BN (the conv input after the
            BN shift, so zero padding needs no border bias)
+  * "f16w1": input stored as one fp16; weights as ONE fp16 (RNE); one product hw*x
 The border-class bias (folded BN) is exact.  The conv0 output (layer 0) and every
 layer output are stored in the format of the layer that reads them as input.
 Reports the worst |logit - float64 reference| over the res golden fixtures and
@@ -65,6 +66,8 @@ def layer_conv(x, W, mean, var, d, scheme):
         hw, lw = split(Ws, f16)
         xc = f16(x)          # the conv reads one fp16 (f16c: the hi half)
         return conv(xc, hw + lw, d) - bias
+    if scheme == "f16w1":
+        return conv(f16(x), f16(Ws), d) - bias
     if scheme == "f16s":
         hw, lw = split(Ws, f16)
         u = f16(x - mean.astype(np.float64)[None, :, None, None])
@@ -79,7 +82,7 @@ def store(x, scheme):
     if scheme == "x3":
         h, l = split(x, bf16)
         return h + l
-    if scheme == "f16":
+    if scheme in ("f16", "f16w1"):
         return f16(x)
     if scheme in ("f16c", "f16s"):
         h, l = split(x, f16)
@@ -98,7 +101,7 @@ def fwd(params, cfg, x, schemes):
     old = y
     for i in range(1, L + 1):
         sc = schemes[i]
-        xin = store(cur, sc) if sc != "f16" else f16(cur)
+        xin = store(cur, sc) if sc not in ("f16", "f16w1") else f16(cur)
         if i == 1 or (i - 1) % 2 == 0 and i > 1:
             # cur is a residual-stream tensor (conv0 output or an even layer's sum):
             # the residual of layer i+1 reads the stored value
@@ -147,7 +150,7 @@ def evaluate(all_cases, scheme_fn):
 if __name__ == "__main__":
     cs = cases(int(os.environ.get("NRAND", "2")))
     only = os.environ.get("ONLY")
-    for sch in ("x3", "f16", "f16c", "f16s"):
+    for sch in ("x3", "f16", "f16c", "f16s", "f16w1"):
         if only and sch not in only.split(","):
             continue
         w, rows = evaluate(cs, lambda L, s=sch: {i: s for i in range(1, L + 1)})

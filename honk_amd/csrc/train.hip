@@ -970,6 +970,70 @@ __host__ __device__ inline int twd_nchunk(int C, int W, int TH) {
   return (C * g.PS / 4 + C * twd_ds(TH, W) / 4 + 63) / 64 * 64;
 }
 
+// The staging of one weight-gradient tile (wgrad3x3d_kernel, wgrad3x3q_kernel): per
+// lane and DMA instruction i, chunk e -> x chunk (plane c, row rr: image row hr + rr d)
+// or dy chunk (plane o, band row jr: image row r + (k0 + jr) d), as the byte offset in
+// its clip tensor at row 0 and the band row; kind 0 = zero chunk
+struct TwdStage {
+  int cbase[TWD_ITER], crow[TWD_ITER], ckind[TWD_ITER];
+};
+__device__ __forceinline__ void twd_stage_init(TwdStage& s, int C, int H, int W, int TH, const TdGeo& G, int wave,
+                                               int lane) {
+  const int DS = twd_ds(TH, W), XF = C * G.PS, nch = twd_nchunk(C, W, TH);
+#pragma unroll
+  for (int i = 0; i < TWD_ITER; ++i) {
+    const int e = (wave * TWD_ITER + i) * 64 + lane, f = e * 4;
+    s.cbase[i] = 0;
+    s.crow[i] = 0;
+    s.ckind[i] = 0;
+    if (e < nch && f < XF) {
+      const int c = f / G.PS, rem = f - c * G.PS, rr = rem / G.Wr, col = rem - rr * G.Wr - TD_PAD;
+      if (rr < G.R && col >= 0 && col < W) {
+        s.cbase[i] = (c * H * W + col) * 4;
+        s.crow[i] = rr - 1;
+        s.ckind[i] = 1;
+      }
+    } else if (e < nch && f - XF < C * DS) {
+      const int g = f - XF, o = g / DS, rem = g - o * DS, jr = rem / W, col = rem - jr * W;
+      if (jr < TH) {
+        s.cbase[i] = (o * H * W + col) * 4;
+        s.crow[i] = jr;
+        s.ckind[i] = 2;
+      }
+    }
+  }
+}
+// DMA of tile `tile` (x band + dy band of one clip) into buf
+__device__ __forceinline__ void twd_issue(const TwdStage& s, const WgradArgs& a, int C, int H, int W, int d, int tile,
+                                          float* buf, int wave) {
+  const int b = tile / a.g.nband;
+  int r, k0, th;
+  band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
+  const size_t clip = (size_t)C * H * W;
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (size_t)b * clip), (short)0, (int)(clip * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.dy + (size_t)b * clip), (short)0, (int)(clip * 4), 0x00020000);
+  const int hb = r + k0 * d;
+#pragma unroll
+  for (int i = 0; i < TWD_ITER; ++i) {
+    const int h = hb + s.crow[i] * d;
+    const bool ok = s.ckind[i] != 0 && h >= 0 && h < H && (s.ckind[i] == 1 || s.crow[i] < th);
+    const unsigned voff = ok ? (unsigned)(s.cbase[i] + h * W * 4) : 0x80000000u;
+    // one LDS slot per lane: a lane's chunk comes from dy (rd) or x / zeros (rx); the
+    // instruction that straddles the x / dy boundary runs twice under complementary
+    // exec masks, every slot written once
+    if (s.ckind[i] == 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rd, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TWD_ITER + i) * 256)),
+          16, voff, 0, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rx, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TWD_ITER + i) * 256)),
+          16, voff, 0, 0, 0);
+  }
+}
+
 // FW, FD, FTH (all > 0): compile-time tile geometry, as conv3x3d_kernel's
 template <int C, int FW = 0, int FD = 0, int FTH = 0>
 __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
@@ -983,7 +1047,6 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   const int d = FIX ? FD : a.g.d, W = FIX ? FW : a.W, H = a.H, TH = FIX ? FTH : a.g.TH;
   const TdGeo G = td_geo(C, W, TH);
   const int DS = twd_ds(TH, W), XF = C * G.PS;  // dy planes start at float XF
-  const int nch = twd_nchunk(C, W, TH);
   int joff[NJ];
 #pragma unroll
   for (int n = 0; n < NJ; ++n) {
@@ -998,61 +1061,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   for (int n = 0; n < NJ; ++n) acc[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int h = 0; h < NH; ++h) acc4[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  // per lane and DMA instruction i: chunk e -> x chunk (plane c, row rr: image row
-  // hr + rr d) or dy chunk (plane o, band row jr: image row r + (k0 + jr) d), as the
-  // byte offset in its clip tensor at row 0 and the band row; kind 0 = zero chunk
-  int cbase[TWD_ITER], crow[TWD_ITER], ckind[TWD_ITER];
-#pragma unroll
-  for (int i = 0; i < TWD_ITER; ++i) {
-    const int e = (wave * TWD_ITER + i) * 64 + lane, f = e * 4;
-    cbase[i] = 0;
-    crow[i] = 0;
-    ckind[i] = 0;
-    if (e < nch && f < XF) {
-      const int c = f / G.PS, rem = f - c * G.PS, rr = rem / G.Wr, col = rem - rr * G.Wr - TD_PAD;
-      if (rr < G.R && col >= 0 && col < W) {
-        cbase[i] = (c * H * W + col) * 4;
-        crow[i] = rr - 1;
-        ckind[i] = 1;
-      }
-    } else if (e < nch && f - XF < C * DS) {
-      const int g = f - XF, o = g / DS, rem = g - o * DS, jr = rem / W, col = rem - jr * W;
-      if (jr < TH) {
-        cbase[i] = (o * H * W + col) * 4;
-        crow[i] = jr;
-        ckind[i] = 2;
-      }
-    }
-  }
+  TwdStage stg;
+  twd_stage_init(stg, C, H, W, TH, G, wave, lane);
   const int ntile = a.B * a.g.nband;
-  const size_t clip = (size_t)C * H * W;
-  auto issue = [&](int tile, float* buf) {
-    const int b = tile / a.g.nband;
-    int r, k0, th;
-    band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
-    const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (size_t)b * clip), (short)0, (int)(clip * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rd =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.dy + (size_t)b * clip), (short)0, (int)(clip * 4), 0x00020000);
-    const int hb = r + k0 * d;
-#pragma unroll
-    for (int i = 0; i < TWD_ITER; ++i) {
-      const int h = hb + crow[i] * d;
-      const bool ok = ckind[i] != 0 && h >= 0 && h < H && (ckind[i] == 1 || crow[i] < th);
-      const unsigned voff = ok ? (unsigned)(cbase[i] + h * W * 4) : 0x80000000u;
-      // one LDS slot per lane: a lane's chunk comes from dy (rd) or x / zeros (rx); the
-      // instruction that straddles the x / dy boundary runs twice under complementary
-      // exec masks, every slot written once
-      if (ckind[i] == 2)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rd, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TWD_ITER + i) * 256)),
-            16, voff, 0, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rx, (__attribute__((address_space(3))) void*)(buf + __builtin_amdgcn_readfirstlane((wave * TWD_ITER + i) * 256)),
-            16, voff, 0, 0, 0);
-    }
-  };
+  auto issue = [&](int tile, float* buf) { twd_issue(stg, a, C, H, W, d, tile, buf, wave); };
   float* buf0 = tdl;
   float* buf1 = tdl + TWD_BUF / 4;
   if ((int)blockIdx.x < ntile) issue(blockIdx.x, buf0);
@@ -1137,6 +1149,215 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
       for (int w = 0; w < 8; ++w) v += tdl[(16 * w + i) * NJP + j];
       if (o < C) pb[o * K9 + j] = v;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------- //
+// wgrad3x3q_kernel<C> (16 < C <= 20, d <= 4, W a multiple of 4): the weight gradient
+// as one rank-1 update per pixel, dW[o][j] += dy[o][p] x_j[p] (j = 9 ci + t), on
+// broadcast 4x4x1 blocks only -- conv3x3d_kernel's scheme turned around: block b of
+// a v_mfma_f32_4x4x1_16b_f32 multiplies the 4 outputs o = 4 g .. 4 g + 3 (A, broadcast
+// from the block that holds them) by the 4 columns j = 64 h + 4 b .. 64 h + 4 b + 3 (B,
+// lane = column), so one pixel is NG x NH = 5 x 3 MFMAs of 8 cycles over 20 x 192
+// padded outputs (0.85 of the pipe useful for 19 maps; wgrad3x3d's 16x16x4 + 4x4x1 mix
+// is 0.91 but needs two transposed operand copies).  A k-step is 4 pixels of one row (W
+// % 4 = 0): its operands are 2 A registers (dy of (g, q) in block 4 g + q; g = 4 in
+// block q of the second) and NH x 4 B values (x of column j at pixels q = 0..3: two
+// ds_read2_b32 per h at immediate offsets), 8 LDS instructions for 60 MFMAs, read one
+// step ahead (no address arithmetic but 5 adds of a wave-uniform base).  Staging, tile
+// loop and the per-workgroup partials as wgrad3x3d_kernel; every output is the same
+// sequence of fp32 FMAs over the wave's pixels as there (bit-identical).
+//   HY (hybrid): outputs 0..15 on 16x16x4 tiles instead (lane (kk, i16): dy(o = i16) and
+// x(j = 16 n + i16) at pixel 4 s + kk, one ds_read_b32 each: 11 tiles for 171 columns),
+// outputs 16..19 on the 4x4x1 blocks as above -- 11 x 36 + 12 x 10 cycles per step
+// against 60 x 10 (measured issue rates, exp/mfma44.hip), 12 more reads.  Measured no
+// faster on res26-narrow's tiles (0.379 vs 0.382 ms per 4096-clip call) and slower on
+// 40-pixel maps (0.48 vs 0.41 ms, exp/wgrad_ab.py): kept for A/B only (HONK_WGRAD=h).
+// ---------------------------------------------------------------------------- //
+template <int C, bool HY, int FW = 0, int FD = 0, int FTH = 0>
+__global__ __launch_bounds__(512, 1) void wgrad3x3q_kernel(WgradArgs a) {
+  static_assert(C > 16 && C <= 20, "wgrad3x3q_kernel: 16 < C <= 20");
+  constexpr int K9 = 9 * C, NH = (K9 + 63) / 64, NG = (C + 3) / 4, NJP = 64 * NH, NJ = (K9 + 15) / 16;
+  static_assert(8 * 4 * NG * NJP <= 2 * TWD_BUF / 4, "wgrad3x3q_kernel: partials exceed the LDS buffers");
+  static_assert(16 * NJ <= NJP, "wgrad3x3q_kernel: tile columns exceed the partial rows");
+  __shared__ __attribute__((aligned(16))) float tdl[2 * TWD_BUF / 4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr bool FIX = FW > 0 && FD > 0 && FTH > 0;
+  const int d = FIX ? FD : a.g.d, W = FIX ? FW : a.W, H = a.H, TH = FIX ? FTH : a.g.TH;
+  const TdGeo G = td_geo(C, W, TH);
+  const int DS = twd_ds(TH, W), XF = C * G.PS;  // dy planes start at float XF
+  // B: column j = 64 h + lane -> x(ci, tap t) relative to the pixel's slot (columns past
+  // K9 read column K9 - 1: their products land in discarded outputs)
+  int boff[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int j = min(64 * h + lane, K9 - 1), ci = j / 9, t = j - 9 * ci;
+    boff[h] = ci * G.PS + (t / 3) * G.Wr + (t % 3) * d + TD_PAD - d;
+  }
+  // A: lane 4 b + i of register 0 holds dy(o = 4 g + i, pixel q) with block b = 4 g + q;
+  // register 1 holds o = 16 + i for two k-steps, this wave's s (block q, lanes < 16) and
+  // s + 8 (block 4 + q, lanes 16..31: pixel + 32).  Rows o >= C (discarded) read o = C - 1.
+  const int q = (lane >> 2) & 3;
+  const int aoff0 = (4 * (lane >> 4) + (lane & 3)) * DS + q;
+  const int o1 = min(16 + (lane & 3), C - 1);
+  const int aoff1 = XF + o1 * DS, apx1 = q + ((lane >> 4) & 1) * 32;
+  // HY: lane (kk, i16) of the 16x16x4 operands: dy(o = i16) and x(j = 16 n + i16) at pixel + kk
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int aoff16 = XF + i16 * DS + kk;
+  int boff16[HY ? NJ : 1];
+#pragma unroll
+  for (int n = 0; n < (HY ? NJ : 1); ++n) {
+    const int j = min(16 * n + i16, K9 - 1), ci = j / 9, t = j - 9 * ci;
+    boff16[n] = ci * G.PS + (t / 3) * G.Wr + (t % 3) * d + TD_PAD - d + kk;
+  }
+  f32x4_t acc[NG][NH], acc16[HY ? NJ : 1];
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc[g][h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int n = 0; n < (HY ? NJ : 1); ++n) acc16[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  TwdStage stg;
+  twd_stage_init(stg, C, H, W, TH, G, wave, lane);
+  const int ntile = a.B * a.g.nband;
+  float* buf0 = tdl;
+  float* buf1 = tdl + TWD_BUF / 4;
+  if ((int)blockIdx.x < ntile) twd_issue(stg, a, C, H, W, d, blockIdx.x, buf0, wave);
+  struct Ops {
+    float a0, b[4][NH], b16[HY ? NJ : 1];
+  };
+  int it = 0;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x, ++it) {
+    float* cur = (it & 1) ? buf1 : buf0;
+    float* nxt = (it & 1) ? buf0 : buf1;
+    td_wait_vm0();
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntile) twd_issue(stg, a, C, H, W, d, tile + gridDim.x, nxt, wave);
+    const int b = tile / a.g.nband;
+    int r, k0, th;
+    band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
+    const int nks = th * W / 4;
+    // the load cursor: k-step ls = pixel 4 ls of the band, at (lrow, lcol); this wave's
+    // steps are wave, wave + 8, ..
+    int lrow = (4 * wave) / W, lcol = 4 * wave - lrow * W;
+    // 7 LDS instructions per step (register 1 every other step): with the next step's
+    // in flight, at most 15 outstanding -- the lgkmcnt range, so each step waits for its
+    // own reads only
+    auto ld = [&](Ops& o) {
+      const float* xp = cur + lrow * G.Wr + lcol;
+      if constexpr (HY) {
+        o.a0 = cur[aoff16 + lrow * W + lcol];
+#pragma unroll
+        for (int n = 0; n < NJ; ++n) o.b16[n] = xp[boff16[n]];
+      } else {
+        o.a0 = cur[XF + aoff0 + lrow * W + lcol];
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o.b[u][h] = xp[boff[h] + u];
+      lcol += 32;
+      while (lcol >= W) {
+        lcol -= W;
+        ++lrow;
+      }
+    };
+    const int npx1 = th * W - 1;
+    auto ld1 = [&](int s) { return cur[aoff1 + min(4 * s + apx1, npx1)]; };
+    // a step's operands are complete when it starts (read a step earlier); the reads of
+    // the next step go out after its first pixel's 15 MFMAs (`next`), so they never
+    // share the lgkm counter with reads still awaited
+    auto step = [&](const Ops& o, float a1, auto ab, auto&& next) {
+      if constexpr (HY) {
+        // 16x16x4 tile n, then the 4x4x1 block of (pixel u, h) = divmod(n, NH), in turn;
+        // the next step's reads after the first 3 + 3
+        static_for<4 * NH>([&](auto m) {
+          constexpr int u = m / NH, h = m % NH;
+          if constexpr (m < NJ) acc16[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a0, o.b16[m], acc16[m], 0, 0, 0);
+          acc[NG - 1][h] =
+              __builtin_amdgcn_mfma_f32_4x4x1f32(a1, o.b[u][h], acc[NG - 1][h], 4, decltype(ab)::value + u, 0);
+          if constexpr (m == NH - 1) {
+            __builtin_amdgcn_sched_barrier(0);
+            next();
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        });
+        return;
+      }
+      static_for<4>([&](auto u) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          static_for<NG>([&](auto g) {
+            if constexpr (g < 4)
+              acc[g][h] = __builtin_amdgcn_mfma_f32_4x4x1f32(o.a0, o.b[u][h], acc[g][h], 4, 4 * g + u, 0);
+            else
+              acc[g][h] = __builtin_amdgcn_mfma_f32_4x4x1f32(a1, o.b[u][h], acc[g][h], 4, decltype(ab)::value + u, 0);
+          });
+        }
+        if constexpr (u == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          next();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
+    };
+    // four steps per trip: register 1 alternates between a1a and a1b without a copy
+    Ops e, o;
+    float a1a = 0.f, a1b = 0.f;
+    if (wave < nks) {
+      ld(e);
+      a1a = ld1(wave);
+    }
+    constexpr std::integral_constant<int, 0> B0{};
+    constexpr std::integral_constant<int, 4> B4{};
+    for (int s = wave; s < nks; s += 32) {
+      step(e, a1a, B0, [&] {
+        if (s + 8 < nks) ld(o);
+      });
+      if (s + 8 >= nks) break;
+      step(o, a1a, B4, [&] {
+        if (s + 16 < nks) {
+          ld(e);
+          a1b = ld1(s + 16);
+        }
+      });
+      if (s + 16 >= nks) break;
+      step(e, a1b, B0, [&] {
+        if (s + 24 < nks) ld(o);
+      });
+      if (s + 24 >= nks) break;
+      step(o, a1b, B4, [&] {
+        if (s + 32 < nks) {
+          ld(e);
+          a1a = ld1(s + 32);
+        }
+      });
+    }
+  }
+  td_wait_vm0();
+  __syncthreads();
+  // per-wave partials [wave][4 g + i][j], summed in wave order
+#pragma unroll
+  for (int g = HY ? NG - 1 : 0; g < NG; ++g)
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tdl[(wave * 4 * NG + 4 * g + i) * NJP + 64 * h + lane] = acc[g][h][i];
+  if constexpr (HY) {
+#pragma unroll
+    for (int n = 0; n < NJ; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tdl[(wave * 4 * NG + 4 * kk + i) * NJP + 16 * n + i16] = acc16[n][i];
+  }
+  __syncthreads();
+  float* pb = a.part + (size_t)blockIdx.x * C * K9;
+  for (int idx = tid; idx < C * K9; idx += 512) {
+    const int o = idx / K9, j = idx - o * K9;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += tdl[(4 * NG * w + o) * NJP + j];
+    pb[idx] = v;
   }
 }
 
@@ -1876,7 +2097,17 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
   a.g = wp.g;
   const int grid = wp.grid;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (wp.dma && train::twd_fixed(a)) hipLaunchKernelGGL((train::wgrad3x3d_kernel<19, 20, 1, 17>), dim3(grid), dim3(512), 0, st, a);
+  // HONK_WGRAD=d: wgrad3x3d_kernel instead of wgrad3x3q_kernel (A/B, tests)
+  const char* we = getenv("HONK_WGRAD");
+  const bool wq = !(we && we[0] == 'd');
+  const bool wh = we && we[0] == 'h';  // HONK_WGRAD=h: the hybrid (16x16x4 for outputs 0..15)
+  if (wp.dma && wq && wh && train::twd_fixed(a))
+    hipLaunchKernelGGL((train::wgrad3x3q_kernel<19, true, 20, 1, 17>), dim3(grid), dim3(512), 0, st, a);
+  else if (wp.dma && wq && wh) hipLaunchKernelGGL((train::wgrad3x3q_kernel<19, true>), dim3(grid), dim3(512), 0, st, a);
+  else if (wp.dma && wq && train::twd_fixed(a))
+    hipLaunchKernelGGL((train::wgrad3x3q_kernel<19, false, 20, 1, 17>), dim3(grid), dim3(512), 0, st, a);
+  else if (wp.dma && wq) hipLaunchKernelGGL((train::wgrad3x3q_kernel<19, false>), dim3(grid), dim3(512), 0, st, a);
+  else if (wp.dma && train::twd_fixed(a)) hipLaunchKernelGGL((train::wgrad3x3d_kernel<19, 20, 1, 17>), dim3(grid), dim3(512), 0, st, a);
   else if (wp.dma) hipLaunchKernelGGL((train::wgrad3x3d_kernel<19>), dim3(grid), dim3(512), 0, st, a);
   else if (wp.mfma) hipLaunchKernelGGL((train::wgrad3x3m_kernel<19>), dim3(grid), dim3(256), 0, st, a);
   else if (c == 19) hipLaunchKernelGGL((train::wgrad3x3_kernel<19>), dim3(grid), dim3(512), 0, st, a);

@@ -358,3 +358,29 @@ def test_fixed_geometry_instances_bitwise(monkeypatch):
     assert torch.equal(l1, l2)
     for k in g1:
         assert torch.equal(g1[k], g2[k]), k
+
+
+@pytest.mark.parametrize("B,H,W,d", [(3, 50, 20, 1), (2, 101, 40, 2), (3, 101, 40, 4), (300, 50, 20, 1), (2, 7, 4, 1),
+                                     (5, 25, 12, 3)])
+def test_wgrad_kernels_bitwise(monkeypatch, B, H, W, d):
+    """The weight-gradient kernels of the LDS-DMA path: wgrad3x3q_kernel (all outputs on
+    broadcast 4x4x1 blocks, the default), its hybrid (HONK_WGRAD=h: outputs 0..15 on
+    16x16x4 tiles) and wgrad3x3d_kernel (HONK_WGRAD=d) run every output's fp32 FMAs over
+    a wave's pixels in the same order: bit-identical, fixed-geometry instance included
+    (res26-narrow's 50 x 20 maps), and within 1e-5 of float64."""
+    g = torch.Generator(device=DEV).manual_seed(11 + H + d)
+    x = torch.randn(B, 19, H, W, device=DEV, generator=g)
+    dy = torch.randn(B, 19, H, W, device=DEV, generator=g)
+    outs = {}
+    for k in ("q", "h", "d"):
+        if k == "q":
+            monkeypatch.delenv("HONK_WGRAD", raising=False)
+        else:
+            monkeypatch.setenv("HONK_WGRAD", k)
+        outs[k] = hc._wgrad(x, dy, d=d)
+    assert torch.equal(outs["q"], outs["d"])
+    assert torch.equal(outs["h"], outs["d"])
+    n = min(B, 16)
+    ref = torch.nn.grad.conv2d_weight(x[:n].double(), (19, 19, 3, 3), dy[:n].double(), padding=d, dilation=d)
+    monkeypatch.delenv("HONK_WGRAD", raising=False)
+    assert _rel(hc._wgrad(x[:n].contiguous(), dy[:n].contiguous(), d=d), ref) < 1e-5
