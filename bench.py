@@ -319,6 +319,9 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
             if k == "block16p_kernel":
                 per_clip += 3 * act
                 layer += 2
+            elif k == "block16n_kernel":  # the whole stack: the conv0 output read once
+                per_clip += act
+                layer += L
             else:
                 per_clip += act * (1 + (1 if layer % 2 == 0 else 0) + (1 if layer < L else 0))
                 layer += 1
@@ -326,7 +329,8 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
         traffic = load_traffic(f"{dom}_{tag}", clips, model)
         what = {"block16p_kernel": "fused odd + even layer pair", "block16w_kernel": "weight-stationary layer",
                 "block16l_kernel": "last layer on the pair's streaming machinery, fused channel sums",
-                "block16r_kernel": "row-band layer"}
+                "block16r_kernel": "row-band layer",
+                "block16n_kernel": "every block layer of a clip, activations resident in LDS"}
         kname = (" + ".join(f"honk::res::{k}<..., {tag}> x{plan.count(k)} ({what[k]})"
                             for k in sorted(set(plan), key=plan.index))
                  + " per chunk: dilated 3x3 convs, "

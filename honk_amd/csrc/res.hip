@@ -525,6 +525,7 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 #include "res_bf16r.inc"
 #include "res_bf16w.inc"
 #include "res_bf16p.inc"
+#include "res_bf16n.inc"
 
 // --------------------------------------------------------------------------- //
 // conv0 on the matrix cores (the bf16 / bf16x3 / f16x2 paths): 1 -> CP 3x3 pad 1,
@@ -1227,6 +1228,41 @@ static int launch_conv0_16(const Layout& L, const float* x, void* out, const flo
   else return launch_conv0<__bf16, FM == 1, ONES>(L, x, (__bf16*)out, w0, n, st);
 }
 
+// the whole-stack kernel (res_bf16n.inc) takes the model: bf16, every layer at
+// dilation 1, a zero-padding channel for the folded bias, 2 or 3 out-tiles, a map
+// whose image fits its LDS slot, at least one m-tile per wave.  HONK_RES_KERNEL=r / w / p
+// forces the per-layer kernels.
+static bool use_n_kernel(const Layout& L, const honk_res_desc* d, int FM) {
+  if (const char* e = getenv("HONK_RES_KERNEL"))
+    if (e[0] == 'r' || e[0] == 'w' || e[0] == 'p') return false;
+  if (FM != 0 || L.L < 1 || L.C >= L.CP || (L.NT != 2 && L.NT != 3)) return false;
+  for (int i = 1; i <= L.L; ++i)
+    if (dil_of(d, i) != 1) return false;
+  if (!g16n_fits(L.NT, L.H, L.W)) return false;
+  return (L.H * L.W + 15) / 16 >= 4;
+}
+
+template <int NT>
+static int launch_block16n(const Layout& L, const __bf16* in, const float* frb, size_t frl, float* chsum, int64_t n,
+                           hipStream_t st) {
+  Block16NArgs a;
+  a.in = in;
+  a.wfrag = (const char*)frb;
+  a.wstride = (int)(frl * sizeof(float));
+  a.chsum = chsum;
+  a.nclips = (int)n;
+  a.H = L.H;
+  a.W = L.W;
+  a.nL = L.L;
+  int grid = cu_count();
+  if (grid > n) grid = (int)n;
+  TimedLaunch tl(st, 2.0 * L.H * L.W * L.C * L.C * 9 * L.L * (double)n);
+  hipLaunchKernelGGL((block16n_kernel<NT>), dim3(grid), dim3(256), 0, st, a);
+  HONK_LAUNCH_CHECK("res block16n_kernel");
+  tl.done(st);
+  return HONK_OK;
+}
+
 // bf16 driver: same schedule as the fp32 one (R / X0 / X1 buffers, fused mean)
 // bf16 schedule: activations stay pre-BN (see res_bf16.inc), so one residual
 // stream R (conv0 output, then every even layer's sum, in place) and one odd-layer
@@ -1249,6 +1285,22 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
     return fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
                 "(use precision f32)", L.W);
   int rc;
+  if (use_n_kernel(L, d, FM)) {
+    // conv0 -> R, then the whole block stack per clip in LDS, then the head
+    for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
+      const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
+      rc = launch_conv0_16<0, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
+      if (rc) return rc;
+      rc = L.NT == 3 ? launch_block16n<3>(L, R, frb, frl, chsum, n, st) : launch_block16n<2>(L, R, frb, frl, chsum, n, st);
+      if (rc) return rc;
+      const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
+      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+                         packed + L.off_bout, logits + c0 * L.NL, 4, L.H * L.W, L.C, L.CP, L.NL, bn_last,
+                         bn_last + L.CP);
+      HONK_LAUNCH_CHECK("res tail_sum_kernel (whole stack)");
+    }
+    return HONK_OK;
+  }
   const bool wpath = use_w_kernel(L, d, FM);
   if (!wpath && FM == 2)
     return fail(HONK_ERR_UNSUPPORTED, "f16x2 runs on the weight-stationary / pair kernels only: %d maps, %dx%d "
@@ -1446,6 +1498,10 @@ int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, i
   }
   const int FM = fmt_of(L.prec), SP = sp_of(FM);
   if (plan_block16r(L, SP).TH == 0) return fail(HONK_ERR_UNSUPPORTED, "width beyond the row-band staging plan");
+  if (use_n_kernel(L, d, FM)) {
+    put(HONK_KERNEL_NET);
+    return cnt;
+  }
   if (!use_w_kernel(L, d, FM)) {
     if (FM == 2) return fail(HONK_ERR_UNSUPPORTED, "f16x2: outside the weight-stationary / pair kernels' envelope");
     for (int i = 1; i <= L.L; ++i) put(HONK_KERNEL_ROWBAND);

@@ -87,6 +87,7 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch);
 #define HONK_KERNEL_WSTAT 3     /* bf16 / bf16x3 weight-stationary layer (block16w_kernel) */
 #define HONK_KERNEL_PAIR 4      /* fused odd + even layer pair (block16p_kernel)           */
 #define HONK_KERNEL_LAST 5      /* last (odd) layer, fused channel sums (block16l_kernel)  */
+#define HONK_KERNEL_NET 6       /* every block layer of a clip in LDS (block16n_kernel), bf16 */
 int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, int32_t* kinds, int32_t max_kinds);
 /*
  * Pack a state_dict into kernel layout.  tensors[] (device, fp32, contiguous),

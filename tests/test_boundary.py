@@ -176,12 +176,12 @@ def test_abi_queries_without_gpu():
     assert n >= 45 * 9 + 13 * 9 * 48 * 48
     assert lib.honk_res_workspace_bytes(d, 10) == 3 * 10 * 101 * 40 * 48 * 4 + 10 * 13 * 4 * 48 * 4
     # bf16: two pre-BN bf16 activation buffers (residual stream + odd-layer output)
-    # + per-(tile, wave, m-tile) channel sums of the last layer; row-band kernel: res15
-    # tiles of 9 rows of one dilation class (8 waves x 3 m-tiles), at most 16 per clip
-    # (dilation 16: 16 classes of 6-7 rows, one tile each)
+    # + per-(tile, wave) channel sums of the last layer (its m-tiles summed per lane,
+    # round 4); row-band kernel: res15 tiles of 9 rows of one dilation class (8 waves),
+    # at most 16 per clip (dilation 16: 16 classes of 6-7 rows, one tile each)
     d16 = _native.ResDesc(n_labels=12, n_maps=45, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
                           height=101, width=40, precision=_native.PRECISIONS["bf16"])
-    assert lib.honk_res_workspace_bytes(d16, 10) == 2 * 10 * 101 * 40 * 48 * 2 + 10 * 16 * 8 * 3 * 48 * 4
+    assert lib.honk_res_workspace_bytes(d16, 10) == 2 * 10 * 101 * 40 * 48 * 2 + 10 * 16 * 8 * 48 * 4
     # bf16x3 past the row-band plan's width: 0 bytes and the reason in honk_last_error
     wide = _native.ResDesc(n_labels=12, n_maps=45, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
                            height=101, width=67, precision=_native.PRECISIONS["bf16x3"])
@@ -230,8 +230,8 @@ def test_res_launch_plan_host_only(monkeypatch):
     """honk_res_launch_plan (host-only): which block kernels a forward launches per
     chunk -- res15 bf16x3 and bf16: six fused odd/even pairs then the last layer on
     the weight-stationary kernel; res26 likewise (last pair unfused: the pair kernel
-    has no channel-sum epilogue); HONK_RES_KERNEL=w / r force single layers; f32 and
-    19-map models keep their kernels."""
+    has no channel-sum epilogue); res8 / res8-narrow bf16: the whole-stack kernel;
+    HONK_RES_KERNEL=w / r force single layers; f32 and 19-map models keep their kernels."""
     from honk_amd import _native
     from honk_amd import model as hm
     lib = _native.load()
@@ -252,7 +252,9 @@ def test_res_launch_plan_host_only(monkeypatch):
     assert plan("res8", "bf16x3") == ["block16p_kernel"] * 2 + ["block16w_kernel"] * 2
     assert plan("res15", "f32") == ["block_kernel"] * 13
     assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16l_kernel"]
-    assert plan("res8", "bf16") == ["block16r_kernel"] * 6  # 13-pixel rows: row-band measured faster
+    assert plan("res8", "bf16") == ["block16n_kernel"]  # the whole stack per clip in LDS
+    assert plan("res8-narrow", "bf16") == ["block16n_kernel"]
+    assert plan("res26-narrow", "bf16") == ["block16r_kernel"] * 24  # 50 x 20 maps: no room for three images
     assert plan("res15-narrow", "bf16x3") == ["block16r_kernel"] * 13
     monkeypatch.setenv("HONK_LAST_KERNEL", "w")
     assert plan("res15", "bf16x3") == ["block16p_kernel"] * 6 + ["block16w_kernel"]
@@ -261,6 +263,7 @@ def test_res_launch_plan_host_only(monkeypatch):
     assert plan("res15", "bf16x3") == ["block16w_kernel"] * 13
     monkeypatch.setenv("HONK_RES_KERNEL", "r")
     assert plan("res15", "bf16x3") == ["block16r_kernel"] * 13
+    assert plan("res8", "bf16") == ["block16r_kernel"] * 6
 
 
 def test_res_launch_plan_errors_raise_with_reason():

@@ -210,3 +210,46 @@ def test_conv0_mfma_vs_valu(monkeypatch, name, prec):
         bar = 1e-4
     assert np.abs(outm - ref).max() <= bar and np.abs(outv - ref).max() <= bar
     assert np.abs(outm - outv).max() <= (2e-5 if prec == "bf16x3" else bar)
+
+
+# the whole-stack kernel (block16n_kernel: every layer of a clip with its activations in
+# LDS): bf16, undilated maps whose image fits its LDS slot -- res8, res8-narrow
+NET_CASES = [("res8", {}, 700), ("res8", {}, 5), ("res8-narrow", {}, 300), ("res8", dict(n_layers=5), 40),
+             ("res8", dict(n_layers=1), 9), ("res8", dict(n_feature_maps=33), 64)]
+
+
+@pytest.mark.parametrize("name,override,B", NET_CASES)
+def test_net_kernel_vs_w(monkeypatch, name, override, B):
+    """Its layers run block16w_kernel's MFMA sequence on the same fragments (the layer
+    outputs are bit-identical); only the channel sums of the last layer add in another
+    order -- so the logits agree to fp32 summation rounding, and sit within the bf16
+    bar of the oracle."""
+    cfg = dict(ref_configs()[name])
+    cfg.update(override)
+    params, x = _case(cfg, B, seed=29)
+    m = _module(cfg, params, name, "bf16")
+    monkeypatch.delenv("HONK_RES_KERNEL", raising=False)
+    assert _native.res_launch_plan(m._desc(101, 40), B) == ["block16n_kernel"]
+    outn = _run(m, x)
+    monkeypatch.setenv("HONK_RES_KERNEL", "w")
+    assert "block16n_kernel" not in _native.res_launch_plan(m._desc(101, 40), B)
+    outw = _run(m, x)
+    np.testing.assert_allclose(outn, outw, atol=2e-5, rtol=2e-5)
+    idx = list(range(0, B, max(1, B // 8)))[:8]
+    ref = orc.forward(params, cfg, x[idx])
+    assert np.abs(outn[idx] - ref).max() <= 0.05
+    assert np.mean(outn[idx].argmax(1) == ref.argmax(1)) >= 0.75
+
+
+def test_net_kernel_batch_invariance(monkeypatch):
+    """A clip's result does not depend on its workgroup or its neighbours: bitwise
+    equal across batch splits and chunk sizes."""
+    monkeypatch.delenv("HONK_RES_KERNEL", raising=False)
+    cfg = dict(ref_configs()["res8"])
+    params, x = _case(cfg, 600, seed=5)
+    m = _module(cfg, params, "res8", "bf16")
+    full = _run(m, x)
+    assert np.array_equal(full, np.concatenate([_run(m, x[:257]), _run(m, x[257:])]))
+    assert np.array_equal(full[3:7], _run(m, x[3:7]))
+    monkeypatch.setenv("HONK_RES_CHUNK", "100")
+    assert np.array_equal(full, _run(m, x))
