@@ -230,8 +230,8 @@ def test_res_launch_plan_host_only(monkeypatch):
     """honk_res_launch_plan (host-only): which block kernels a forward launches per
     chunk -- res15 bf16x3 and bf16: six fused odd/even pairs then the last layer on
     the weight-stationary kernel; res26 likewise (last pair unfused: the pair kernel
-    has no channel-sum epilogue); res8 / res8-narrow bf16: the whole-stack kernel;
-    HONK_RES_KERNEL=w / r force single layers; f32 and 19-map models keep their kernels."""
+    has no channel-sum epilogue); HONK_RES_KERNEL=w / r force single layers, n the
+    whole-stack kernel (res8 / res8-narrow bf16); f32 and 19-map models keep their kernels."""
     from honk_amd import _native
     from honk_amd import model as hm
     lib = _native.load()
@@ -252,9 +252,8 @@ def test_res_launch_plan_host_only(monkeypatch):
     assert plan("res8", "bf16x3") == ["block16p_kernel"] * 2 + ["block16w_kernel"] * 2
     assert plan("res15", "f32") == ["block_kernel"] * 13
     assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16l_kernel"]
-    assert plan("res8", "bf16") == ["block16n_kernel"]  # the whole stack per clip in LDS
-    assert plan("res8-narrow", "bf16") == ["block16n_kernel"]
-    assert plan("res26-narrow", "bf16") == ["block16r_kernel"] * 24  # 50 x 20 maps: no room for three images
+    assert plan("res8", "bf16") == ["block16r_kernel"] * 6  # 13-pixel rows: row-band measured faster
+    assert plan("res26-narrow", "bf16") == ["block16r_kernel"] * 24
     assert plan("res15-narrow", "bf16x3") == ["block16r_kernel"] * 13
     monkeypatch.setenv("HONK_LAST_KERNEL", "w")
     assert plan("res15", "bf16x3") == ["block16p_kernel"] * 6 + ["block16w_kernel"]
@@ -263,7 +262,11 @@ def test_res_launch_plan_host_only(monkeypatch):
     assert plan("res15", "bf16x3") == ["block16w_kernel"] * 13
     monkeypatch.setenv("HONK_RES_KERNEL", "r")
     assert plan("res15", "bf16x3") == ["block16r_kernel"] * 13
-    assert plan("res8", "bf16") == ["block16r_kernel"] * 6
+    monkeypatch.setenv("HONK_RES_KERNEL", "n")  # the whole-stack kernel (opt-in)
+    assert plan("res8", "bf16") == ["block16n_kernel"]
+    assert plan("res8-narrow", "bf16") == ["block16n_kernel"]
+    assert plan("res26-narrow", "bf16") == ["block16r_kernel"] * 24  # 50 x 20 maps: no room for three images
+    assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16l_kernel"]  # dilated: not taken
 
 
 def test_res_launch_plan_errors_raise_with_reason():

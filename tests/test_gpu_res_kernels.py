@@ -213,7 +213,8 @@ def test_conv0_mfma_vs_valu(monkeypatch, name, prec):
 
 
 # the whole-stack kernel (block16n_kernel: every layer of a clip with its activations in
-# LDS): bf16, undilated maps whose image fits its LDS slot -- res8, res8-narrow
+# LDS; opt-in, HONK_RES_KERNEL=n): bf16, undilated maps whose image fits its LDS slot --
+# res8, res8-narrow
 NET_CASES = [("res8", {}, 700), ("res8", {}, 5), ("res8-narrow", {}, 300), ("res8", dict(n_layers=5), 40),
              ("res8", dict(n_layers=1), 9), ("res8", dict(n_feature_maps=33), 64)]
 
@@ -228,7 +229,7 @@ def test_net_kernel_vs_w(monkeypatch, name, override, B):
     cfg.update(override)
     params, x = _case(cfg, B, seed=29)
     m = _module(cfg, params, name, "bf16")
-    monkeypatch.delenv("HONK_RES_KERNEL", raising=False)
+    monkeypatch.setenv("HONK_RES_KERNEL", "n")
     assert _native.res_launch_plan(m._desc(101, 40), B) == ["block16n_kernel"]
     outn = _run(m, x)
     monkeypatch.setenv("HONK_RES_KERNEL", "w")
@@ -244,7 +245,7 @@ def test_net_kernel_vs_w(monkeypatch, name, override, B):
 def test_net_kernel_batch_invariance(monkeypatch):
     """A clip's result does not depend on its workgroup or its neighbours: bitwise
     equal across batch splits and chunk sizes."""
-    monkeypatch.delenv("HONK_RES_KERNEL", raising=False)
+    monkeypatch.setenv("HONK_RES_KERNEL", "n")
     cfg = dict(ref_configs()["res8"])
     params, x = _case(cfg, 600, seed=5)
     m = _module(cfg, params, "res8", "bf16")
