@@ -528,6 +528,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
   float sa[MODE ? C : 1], sb[MODE ? C : 1];  // per-lane statistics (MODE 1 / 2)
 #pragma unroll
   for (int o = 0; o < (MODE ? C : 1); ++o) sa[o] = sb[o] = 0.f;
+  // MODE 1: the lane's sums are of s - piv[o], piv = the lane's first s of the channel,
+  // so a channel whose mean is large against its spread (a residual sum) keeps its
+  // variance digits in fp32; the lane's (count, sums) are turned back into sums of s and
+  // s^2 in double before the cross-lane reduction
+  float piv[MODE == 1 ? C : 1];
+#pragma unroll
+  for (int o = 0; o < (MODE == 1 ? C : 1); ++o) piv[o] = 0.f;
+  int pcnt = 0;  // MODE 1: valid pixels this lane has summed
   // Deferred epilogue: a super tile's outputs (stores, statistics) go out during the
   // MFMAs of the wave's next super tile -- one channel every 8 k -- instead of after
   // its own loop, where the 8 waves (one super tile each per band tile) would all sit
@@ -556,8 +564,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
         } else {
           pyb[(size_t)o * H * W + ppix] = v;
         }
-        sa[o] += sv;
-        sb[o] += sv * sv;
+        piv[o] = pcnt == 0 ? sv : piv[o];
+        const float dv = sv - piv[o];
+        sa[o] += dv;
+        sb[o] += dv * dv;
+        if (o == C - 1) ++pcnt;
       } else {
         pyb[(size_t)o * H * W + ppix] = v;
       }
@@ -641,6 +652,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
 #pragma unroll
     for (int o = 0; o < C; ++o) {
       double u = sa[o], v = sb[o];
+      if constexpr (MODE == 1) {  // sums of s and s^2 from the pivoted ones
+        const double p = piv[o], n = pcnt;
+        v = v + 2.0 * p * u + n * p * p;
+        u = u + n * p;
+      }
 #pragma unroll
       for (int m = 32; m >= 1; m >>= 1) {
         u += __shfl_xor(u, m);

@@ -104,6 +104,8 @@ def record(dec: Decisions):
         if k == (1, 1):
             dec.pool.append(None)
         else:
+            # torch's index = the native kernel's routing (ties, -inf, NaN / -NaN windows:
+            # test_gpu_cnn_train.py::test_maxpool_bwd_bitwise_vs_torch)
             dec.pool.append(F.max_pool2d(x.detach(), k, return_indices=True)[1].cpu())
         return orig_pool(self, p, x, native)
 

@@ -84,11 +84,17 @@ def test_wgrad_deterministic():
 
 @pytest.mark.parametrize("k", [(2, 2), (1, 3), (2, 3), (3, 3)])
 def test_maxpool_bwd_bitwise_vs_torch(k):
-    """Integer-valued inputs (many ties), -inf entries, floor-truncated borders: the
-    gradient goes exactly where torch's max_pool2d index puts it."""
+    """Integer-valued inputs (many ties), -inf entries, NaN / -NaN entries (one or
+    several per window), floor-truncated borders: the gradient goes exactly where
+    torch's max_pool2d index puts it -- so tests/decision_replay.py, which records the
+    pool decisions from torch's indices, records the native kernel's own routing."""
     g = torch.Generator().manual_seed(k[0] * 10 + k[1])
     x = torch.randint(-3, 4, (4, 6, 25, 17), generator=g).float()
     x[0, 0, :4, :4] = float("-inf")
+    x[1, 2, 3:6, 3:6] = float("nan")                    # whole windows of NaN
+    x[2, 3, 0, 1] = float("nan")                        # one NaN among ties
+    x[3, 1, 7, 2] = -float("nan")
+    x[3, 1, 8, 2] = float("nan")                        # two NaNs, one window (2 x k)
     gy = torch.randn(4, 6, 25 // k[0], 17 // k[1], generator=g)
     xr = x.clone().requires_grad_(True)
     F.max_pool2d(xr, k).backward(gy)
@@ -96,7 +102,9 @@ def test_maxpool_bwd_bitwise_vs_torch(k):
     pool = torch.nn.MaxPool2d(k)
     assert ct.pool_supported(xd, pool)
     out = ct.max_pool(xd, pool)
-    assert torch.equal(out.detach().cpu(), F.max_pool2d(x, k))
+    ref = F.max_pool2d(x, k)
+    assert torch.equal(out.detach().cpu().nan_to_num(7.5), ref.nan_to_num(7.5))
+    assert torch.equal(out.detach().cpu().isnan(), ref.isnan())
     out.backward(gy.to(DEV))
     assert torch.equal(xd.grad.cpu(), xr.grad)
 

@@ -384,3 +384,31 @@ def test_wgrad_kernels_bitwise(monkeypatch, B, H, W, d):
     ref = torch.nn.grad.conv2d_weight(x[:n].double(), (19, 19, 3, 3), dy[:n].double(), padding=d, dilation=d)
     monkeypatch.delenv("HONK_WGRAD", raising=False)
     assert _rel(hc._wgrad(x[:n].contiguous(), dy[:n].contiguous(), d=d), ref) < 1e-5
+
+
+@pytest.mark.parametrize("keep", [False, True])
+def test_fused_tail_statistics_large_mean(keep):
+    """A residual sum whose mean is large against its spread (s ~ 300 + 0.01 N(0,1)): the
+    fused conv epilogue sums the BatchNorm statistics per lane in fp32 around a pivot
+    (the lane's first value), so mean and variance match the float64 statistics of s
+    (running_mean / running_var after one step) to fp32 rounding -- without the pivot
+    s^2 sums lose the variance's digits."""
+    B, C, H, W = 64, 19, 50, 20
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(B, C, H, W, device=DEV, generator=g) * 0.01
+    w = torch.randn(C, C, 3, 3, device=DEV, generator=g) * 0.1
+    old = 300.0 + torch.randn(B, C, H, W, device=DEV, generator=g) * 0.01
+    bn = torch.nn.BatchNorm2d(C, affine=False, momentum=1.0).to(DEV).train()  # running = batch stats
+    box = {}
+    with torch.no_grad():
+        h = hc.conv3x3(x, w, 1, old=old, box_out=box)
+        out = hc.res_tail(h, old, bn, keep_s=keep, box=box)
+        s = torch.relu(hc._conv(x, w, flip=False, d=1)) + old
+    s64 = s.double()
+    mean = s64.mean(dim=(0, 2, 3))
+    var = s64.var(dim=(0, 2, 3), unbiased=True)
+    assert _rel(bn.running_mean, mean) < 1e-6
+    rv = float(((bn.running_var.double() - var).abs() / var).max())
+    print(f"keep={keep}: running_var rel err {rv:.2e} (var ~ {float(var.mean()):.2e})")
+    assert rv < 1e-3
+    del out
