@@ -95,6 +95,16 @@ _PROTOS = {
     "honk_res_tail_bwd_mask_f32": (ctypes.c_int, [c_f32p] * 4 + [ctypes.c_void_p] + [c_f32p] * 2
                                    + [ctypes.c_int64] + [ctypes.c_int32] * 4
                                    + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_conv3x3_bn_fold_check": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_int32] * 4),
+    "honk_conv3x3_tail_bn_f32": (ctypes.c_int, [c_f32p] * 3 + [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_int32] * 4
+                                 + [c_f32p] * 3 + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_conv3x3_stats_bn_f32": (ctypes.c_int, [c_f32p] * 3 + [ctypes.c_int64] + [ctypes.c_int32] * 6
+                                  + [c_f32p] * 3 + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_conv3x3_wgrad_bn_f32": (ctypes.c_int, [c_f32p, c_f32p, c_f32p, ctypes.c_int64] + [ctypes.c_int32] * 4
+                                  + [c_f32p] * 2 + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_res_tail_bwd_mask_bn_f32": (ctypes.c_int, [c_f32p] * 5 + [ctypes.c_void_p] + [c_f32p] * 2
+                                      + [ctypes.c_int64] + [ctypes.c_int32] * 4
+                                      + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "honk_res_tail_fwd_part_f32": (ctypes.c_int, [c_f32p] * 8 + [ctypes.c_void_p, ctypes.c_int64]
                                    + [ctypes.c_int32] * 4 + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]),
     "honk_res_tail_bwd_part_f32": (ctypes.c_int, [c_f32p] * 7 + [ctypes.c_void_p, ctypes.c_int64]

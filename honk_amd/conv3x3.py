@@ -120,6 +120,7 @@ def _wgrad(x, dy, d=1):
 
 
 STATS_USED = {"fwd": 0, "bwd": 0}   # tails that took the conv epilogue's statistics (tests)
+FOLD_USED = {"n": 0}   # convs that took the layer below's BatchNorm folded in (tests)
 
 
 def _stats_buf(B, C, H, W, d, device):
@@ -128,18 +129,48 @@ def _stats_buf(B, C, H, W, d, device):
     return torch.empty(n, dtype=torch.uint8, device=device) if n else None
 
 
-def _conv_stats(x, w, flip, d, mode, aux, buf):
+def _conv_stats(x, w, flip, d, mode, aux, buf, fold=None):
+    """fold = (mean, invstd): aux (mode 2) holds the layer below's s, read as its
+    BatchNorm output (honk_conv3x3_stats_bn_f32)."""
     x = x.contiguous()
     B, C, H, W = x.shape
     y = torch.empty_like(x)
-    _native.check(_native.load().honk_conv3x3_stats_f32(
+    fm, fi = (fold[0].data_ptr(), fold[1].data_ptr()) if fold is not None else (None, None)
+    _native.check(_native.load().honk_conv3x3_stats_bn_f32(
         x.data_ptr(), w.data_ptr(), y.data_ptr(), B, C, H, W, d, 1 if flip else 0, mode,
-        aux.data_ptr() if aux is not None else None, buf.data_ptr(), buf.numel(), _native.stream_handle(x.device)),
-        "honk_conv3x3_stats_f32")
+        aux.data_ptr() if aux is not None else None, fm, fi, buf.data_ptr(), buf.numel(),
+        _native.stream_handle(x.device)), "honk_conv3x3_stats_bn_f32")
     return y
 
 
+def _wgrad_fold(xs, dy, d, fold):
+    """The weight gradient of a conv whose input is BatchNorm(xs) (xs = the layer
+    below's s, fold = its (mean, invstd)): honk_conv3x3_wgrad_bn_f32."""
+    dy = dy.contiguous()
+    B, C, H, W = xs.shape
+    lib = _native.load()
+    dw = torch.empty(C, C, 3, 3, dtype=torch.float32, device=xs.device)
+    nbytes = lib.honk_conv3x3_wgrad_workspace_bytes(B, C, H, W, d)
+    ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=xs.device)
+    _native.check(lib.honk_conv3x3_wgrad_bn_f32(xs.data_ptr(), dy.data_ptr(), dw.data_ptr(), B, C, H, W, d,
+                                                fold[0].data_ptr(), fold[1].data_ptr(), ws.data_ptr(), nbytes,
+                                                _native.stream_handle(xs.device)), "honk_conv3x3_wgrad_bn_f32")
+    return dw
+
+
 FUSE_TAIL = os.environ.get("HONK_TRAIN_FUSE_TAIL", "1") != "0"   # tests compare both
+# a block's train BatchNorm folded into the next conv (its forward, input-gradient and
+# weight-gradient kernels make y from s where they read it; the tail writes no y)
+FOLD_BN = os.environ.get("HONK_TRAIN_FOLD_BN", "0") == "1"
+
+
+def fold_supported(h, d_next) -> bool:
+    """The tail of conv output h can hand its BatchNorm to a next conv of dilation
+    d_next (FUSE_TAIL's epilogue path, and the kernels of honk_conv3x3_bn_fold_check)."""
+    if not (FUSE_TAIL and FOLD_BN and h.is_cuda and h.dim() == 4):
+        return False
+    B, C, H, W = h.shape
+    return _native.load().honk_conv3x3_bn_fold_check(B, C, H, W, int(d_next)) == 0
 
 
 class _Conv3x3(torch.autograd.Function):
@@ -150,14 +181,38 @@ class _Conv3x3(torch.autograd.Function):
     returned tensor then holds s, which only the tail reads (autograd still sees h: the
     gradient it hands back is the tail's gh); box_in (the box of the tail whose output x
     is) -> the input-gradient conv sums that tail's backward statistics (of dx and
-    dx * x) into box_in["bwd"] = (buffer, dx)."""
+    dx * x) into box_in["bwd"] = (buffer, dx).  box_in["fold"] = (s, mean, invstd): that
+    tail folded its BatchNorm into this conv -- x is a placeholder of y's shape (never
+    read) and the kernels read y = (s - mean) * invstd from s."""
 
     @staticmethod
     def forward(ctx, x, w, d, old, box_out, box_in):
         w = w.contiguous()
-        ctx.save_for_backward(x, w)
+        fold = box_in.pop("fold", None) if box_in is not None else None
+        ctx.fold = fold is not None
+        if fold is not None:
+            xs, fm, fi = fold
+            ctx.save_for_backward(xs, w, fm, fi)
+        else:
+            ctx.save_for_backward(x, w)
         ctx.dil = d
         ctx.box_in = box_in
+        if fold is not None:
+            FOLD_USED["n"] += 1
+            if box_out is None or not FUSE_TAIL:
+                raise RuntimeError("honk_amd: a folded BatchNorm needs the fused tail epilogue")
+            B, C, H, W = xs.shape
+            buf = _stats_buf(B, C, H, W, d, xs.device)
+            box_out["fwd"] = (buf, d)
+            oc = old.contiguous() if old is not None else None
+            s = torch.empty_like(xs)
+            mask = torch.empty(B, H, W, dtype=torch.int32, device=xs.device)
+            _native.check(_native.load().honk_conv3x3_tail_bn_f32(
+                xs.data_ptr(), w.data_ptr(), s.data_ptr(), mask.data_ptr(), B, C, H, W, d,
+                oc.data_ptr() if oc is not None else None, fm.data_ptr(), fi.data_ptr(), buf.data_ptr(), buf.numel(),
+                _native.stream_handle(xs.device)), "honk_conv3x3_tail_bn_f32")
+            box_out["mask"] = mask
+            return s
         if box_out is not None:
             B, C, H, W = x.shape
             buf = _stats_buf(B, C, H, W, d, x.device)
@@ -179,7 +234,11 @@ class _Conv3x3(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        if ctx.fold:
+            x, w, fm, fi = ctx.saved_tensors   # x: the layer below's s
+            fold = (fm, fi)
+        else:
+            (x, w), fold = ctx.saved_tensors, None
         dy = dy.contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
@@ -187,11 +246,16 @@ class _Conv3x3(torch.autograd.Function):
             B, C, H, W = x.shape
             buf = _stats_buf(B, C, H, W, ctx.dil, x.device) if box is not None else None
             if buf is not None:
-                dx = _conv_stats(dy, w, True, ctx.dil, 2, x.contiguous(), buf)
+                dx = _conv_stats(dy, w, True, ctx.dil, 2, x.contiguous(), buf, fold)
                 box["bwd"] = (buf, dx, dx._version, ctx.dil)
+            elif fold is not None:
+                raise RuntimeError("honk_amd: a folded BatchNorm needs the input-gradient statistics epilogue")
             else:
                 dx = _conv(dy, w, flip=True, d=ctx.dil)
-        dw = _wgrad(x, dy, d=ctx.dil) if ctx.needs_input_grad[1] else None
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad_fold(x, dy, ctx.dil, fold) if fold is not None else _wgrad(x, dy, d=ctx.dil)
+        else:
+            dw = None
         return dx, dw, None, None, None, None
 
 
@@ -244,7 +308,7 @@ class _ResTail(torch.autograd.Function):
     statistics come from those convs' epilogues (honk_res_tail_*_part_f32)."""
 
     @staticmethod
-    def forward(ctx, h, old, running_mean, running_var, momentum, eps, keep_s, box):
+    def forward(ctx, h, old, running_mean, running_var, momentum, eps, keep_s, box, fold=False):
         h = h.contiguous()
         old = old.contiguous() if old is not None else None
         B, C, H, W = h.shape
@@ -258,10 +322,17 @@ class _ResTail(torch.autograd.Function):
             # h holds s = relu(h) [+ old] from the conv's epilogue (and old was read there)
             STATS_USED["fwd"] += 1
             buf, d = box.pop("fwd")
+            # fold: no y -- the next conv reads (s - mean) * invstd from s (box["fold"]);
+            # the returned y is a placeholder of its shape that nothing reads
             _native.check(_native.load().honk_res_tail_fwd_s_f32(
-                h.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean), ptr(running_var),
-                buf.data_ptr(), B, C, H, W, d, momentum, eps, st), "honk_res_tail_fwd_s_f32")
-            ctx.save_for_backward(mask, y, invstd)
+                h.data_ptr(), None if fold else y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
+                ptr(running_var), buf.data_ptr(), B, C, H, W, d, momentum, eps, st), "honk_res_tail_fwd_s_f32")
+            if fold:
+                box["fold"] = (h, mean, invstd)
+                ctx.save_for_backward(mask, h, invstd, mean)
+            else:
+                ctx.save_for_backward(mask, y, invstd)
+            ctx.fold = bool(fold)
             ctx.has_old = old is not None
             ctx.box = box
             ctx.masked = True
@@ -282,6 +353,7 @@ class _ResTail(torch.autograd.Function):
                                                                ptr(running_var), B, C, H * W, momentum, eps,
                                                                ws.data_ptr(), nb, st), "honk_res_tail_fwd_f32")
         ctx.save_for_backward(h, y, invstd)
+        ctx.fold = False
         ctx.has_old = old is not None
         ctx.box = box
         ctx.masked = False
@@ -291,7 +363,8 @@ class _ResTail(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, gs=None):
-        h, y, invstd = ctx.saved_tensors  # (masked: h is the conv epilogue's ReLU mask)
+        # (masked: h is the conv epilogue's ReLU mask; fold: y is the tail's s)
+        h, y, invstd = ctx.saved_tensors[:3]
         B, C, H, W = y.shape
         if gy is None:
             gy = torch.zeros_like(y)
@@ -309,9 +382,17 @@ class _ResTail(torch.autograd.Function):
                 gy = gy.contiguous()
                 buf, _ = _bn_ws(B, C, H * W, y.device)
                 dil = 0
-            _native.check(_native.load().honk_res_tail_bwd_mask_f32(
-                gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(), h.data_ptr(), gh.data_ptr(), ptr(gold),
-                B, C, H, W, dil, buf.data_ptr(), buf.numel(), st), "honk_res_tail_bwd_mask_f32")
+            if ctx.fold:
+                if dil == 0:
+                    raise RuntimeError("honk_amd: a folded BatchNorm's gradient reached the tail without its conv")
+                _native.check(_native.load().honk_res_tail_bwd_mask_bn_f32(
+                    gy.data_ptr(), ptr(gs), y.data_ptr(), ctx.saved_tensors[3].data_ptr(), invstd.data_ptr(),
+                    h.data_ptr(), gh.data_ptr(), ptr(gold), B, C, H, W, dil, buf.data_ptr(), buf.numel(), st),
+                    "honk_res_tail_bwd_mask_bn_f32")
+            else:
+                _native.check(_native.load().honk_res_tail_bwd_mask_f32(
+                    gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(), h.data_ptr(), gh.data_ptr(), ptr(gold),
+                    B, C, H, W, dil, buf.data_ptr(), buf.numel(), st), "honk_res_tail_bwd_mask_f32")
         elif pre is not None and pre[1] is gy and gy._version == pre[2]:
             # the statistics of exactly this gradient, summed by the conv that produced it
             STATS_USED["bwd"] += 1
@@ -325,18 +406,20 @@ class _ResTail(torch.autograd.Function):
                                                                invstd.data_ptr(), h.data_ptr(), gh.data_ptr(),
                                                                ptr(gold), B, C, H * W, ws.data_ptr(), nb, st),
                           "honk_res_tail_bwd_f32")
-        return gh, gold, None, None, None, None, None, None
+        return gh, gold, None, None, None, None, None, None, None
 
 
-def res_tail(h, old, bn, keep_s=False, box=None):
+def res_tail(h, old, bn, keep_s=False, box=None, fold=False):
     """The res block tail in training (model.py:111-118): x = relu(h); x = x + old
     (old not None); old_x = x; x = bn(x) -- one native kernel chain, bit-identical
     to the unfused PyTorch ops (with a statistics box, box["fwd"] from the conv that
     made h: the same ops with the statistics from that conv's epilogue).  Returns
-    bn's output, or (output, old_x) if keep_s."""
+    bn's output, or (output, old_x) if keep_s.  fold (fold_supported, the box's conv
+    epilogue path): bn's output is left to the next conv3x3, which must be called with
+    box_in=box -- the returned output is then a placeholder of its shape."""
     bn.num_batches_tracked.add_(1)
     out = _ResTail.apply(h, old, bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps), bool(keep_s),
-                         box)
+                         box, bool(fold))
     torch.autograd.graph.increment_version(bn.running_mean)
     torch.autograd.graph.increment_version(bn.running_var)
     return out

@@ -127,6 +127,11 @@ struct Conv3Args {
   // mask[b][p] bit o = !(conv[b][o][p] <= 0) (the ReLU's backward mask, torch's
   // threshold_backward; one 32-bit word per pixel, C <= 20)
   unsigned* mask;
+  // the layer below's train BatchNorm folded in (conv3x3d_kernel, may be null): MODE 1
+  // convolves y = (x - fm[c]) fi[c] (x holds that layer's s), MODE 2 reads its aux the
+  // same way -- y is never written to HBM
+  const float* fm = nullptr;
+  const float* fi = nullptr;
 };
 
 typedef float tf2 __attribute__((ext_vector_type(2)));
@@ -409,6 +414,32 @@ __host__ __device__ inline TdGeo td_geo(int C, int W, int TH) {
   return g;
 }
 
+// The folded BatchNorm on a staged tile (conv3x3d_kernel MODE 1, wgrad3x3d/q_kernel):
+// each lane rewrites the 16-B chunks its own LDS-DMA instructions wrote (chunk e = base_e
+// + 64 i at float 4 e; plane c = 4 e / PS), right after its own vmcnt wait and before the
+// tile's barrier -- no barrier of its own.  An in-image x chunk (ok[i]) holds the layer
+// below's s and becomes (s - mean[c]) invstd[c], tail_fwd_kernel's fp32 expression
+// (bit-identical to the y it would have written); pad columns and out-of-image rows stay
+// zero (the conv's zero padding of y).  bnf: mean in [0][c], invstd in [1][c] (LDS).
+template <int N>
+__device__ __forceinline__ void td_bn_fold(float* buf, const float (*bnf)[20], int base_e, int PS,
+                                           const bool (&ok)[N]) {
+  float4 v[N];
+  int c[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    c[i] = 4 * (base_e + 64 * i) / PS;
+    if (ok[i]) v[i] = *(const float4*)(buf + 4 * (base_e + 64 * i));
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (ok[i]) {
+      const float m = bnf[0][c[i]], iv = bnf[1][c[i]];
+      *(float4*)(buf + 4 * (base_e + 64 * i)) =
+          float4{(v[i].x - m) * iv, (v[i].y - m) * iv, (v[i].z - m) * iv, (v[i].w - m) * iv};
+    }
+}
+
 // f(std::integral_constant<int, 0>{}) .. f(std::integral_constant<int, N - 1>{}): a
 // compile-time index (an MFMA's ABID must be a constant)
 template <typename F, int... I>
@@ -465,16 +496,34 @@ __device__ __forceinline__ f32x4_t mfma4_bc(float a, float b, f32x4_t c, int abi
 // FW, FD, FTH (all > 0): the tile geometry (map width, dilation, class rows per tile)
 // fixed at compile time, so every k's operand offset is an immediate of its ds_read
 // (res26-narrow's 20-pixel maps at d = 1); 0: read from the arguments.
-template <int C, int MODE, int FW = 0, int FD = 0, int FTH = 0>
+// FOLD: a.fm / a.fi are set (the folded BatchNorm, Conv3Args::fm; compile-time so the
+// plain instances keep their register allocation)
+template <int C, int MODE, int FW = 0, int FD = 0, int FTH = 0, bool FOLD = false>
 __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
   static_assert(C <= 20, "conv3x3d_kernel: C <= 20");
   constexpr int K = 9 * C, KT = (K + 15) / 16, NG = (C + 3) / 4, PF = 8;  // PF: reads in flight
   __shared__ __attribute__((aligned(16))) float tdl[2 * TD_BUF / 4];
+  __shared__ float bnf[2][20];  // the folded BatchNorm's mean / invstd (a.fm)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr bool FIX = FW > 0 && FD > 0 && FTH > 0;
   const int d = FIX ? FD : a.g.d, W = FIX ? FW : a.W, H = a.H;
   const TdGeo G = td_geo(C, W, FIX ? FTH : a.g.TH);
+  constexpr bool fold = FOLD && MODE != 0;
+  // MODE 2: lane o < C holds channel o's mean / invstd, read out with v_readlane (no
+  // memory operation among the k loop's counted LDS reads)
+  float fmv = 0.f, fiv = 0.f;
+  if (fold) {
+    if (MODE == 1 && tid < C) {
+      bnf[0][tid] = a.fm[tid];
+      bnf[1][tid] = a.fi[tid];
+    }
+    if (MODE == 2 && lane < C) {
+      fmv = a.fm[lane];
+      fiv = a.fi[lane];
+    }
+    __syncthreads();
+  }
   float wt[NG][KT];
 #pragma unroll
   for (int g = 0; g < NG; ++g)
@@ -573,8 +622,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
         pyb[(size_t)o * H * W + ppix] = v;
       }
       if constexpr (MODE == 2) {
+        float yv = pav[o];
+        if (fold) {  // aux is the layer below's s: its y as tail_fwd_kernel makes it (at use: the
+                     // load's latency stays hidden behind a super tile)
+          const float m = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, fmv), o));
+          const float iv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, fiv), o));
+          yv = (yv - m) * iv;
+        }
         sa[o] += v;
-        sb[o] += v * pav[o];
+        sb[o] += v * yv;
       }
     }
   };
@@ -588,6 +644,19 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
     float* cur = (it & 1) ? buf1 : buf0;
     float* nxt = (it & 1) ? buf0 : buf1;
     td_wait_vm0();
+    if (MODE == 1 && fold) {  // the input is the layer below's s: its y in place (own chunks)
+      const int b = tile / a.g.nband;
+      int r, k0, th;
+      band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
+      const int hr = r + (k0 - 1) * d;
+      bool ok[TD_ITER];
+#pragma unroll
+      for (int i = 0; i < TD_ITER; ++i) {
+        const int h = hr + crow[i] * d;
+        ok[i] = cbase[i] >= 0 && h >= 0 && h < H;
+      }
+      td_bn_fold(cur, bnf, wave * TD_ITER * 64 + lane, PS, ok);
+    }
     __syncthreads();  // this tile's DMA landed everywhere; nobody reads nxt any more
     if (tile + (int)gridDim.x < ntile) issue(tile + gridDim.x, nxt);
     const int b = tile / a.g.nband;
@@ -721,6 +790,10 @@ struct WgradArgs {
   float* part;      // [gridDim.x][C][C][9] partial sums
   int B, H, W;
   ClassBands g;
+  // wgrad3x3d/q_kernel, may be null: x holds the layer below's s, the kernel reads its
+  // BatchNorm output (x - fm[c]) fi[c] (Conv3Args::fm)
+  const float* fm = nullptr;
+  const float* fi = nullptr;
 };
 
 // wgrad: 512 threads = NG groups of TG threads (+ idle); group g takes the tile's
@@ -1050,6 +1123,22 @@ __device__ __forceinline__ void twd_issue(const TwdStage& s, const WgradArgs& a,
   }
 }
 
+// td_bn_fold on this lane's x chunks of tile `tile` (kind 1, in-image rows)
+__device__ __forceinline__ void twd_bn_fold(const TwdStage& s, const WgradArgs& a, int H, int d, int tile, float* buf,
+                                            const float (*bnf)[20], int wave, int lane, int PS) {
+  const int b = tile / a.g.nband;
+  int r, k0, th;
+  band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
+  const int hb = r + k0 * d;
+  bool ok[TWD_ITER];
+#pragma unroll
+  for (int i = 0; i < TWD_ITER; ++i) {
+    const int h = hb + s.crow[i] * d;
+    ok[i] = s.ckind[i] == 1 && h >= 0 && h < H;
+  }
+  td_bn_fold(buf, bnf, wave * TWD_ITER * 64 + lane, PS, ok);
+}
+
 // FW, FD, FTH (all > 0): compile-time tile geometry, as conv3x3d_kernel's
 template <int C, int FW = 0, int FD = 0, int FTH = 0>
 __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
@@ -1063,6 +1152,14 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   const int d = FIX ? FD : a.g.d, W = FIX ? FW : a.W, H = a.H, TH = FIX ? FTH : a.g.TH;
   const TdGeo G = td_geo(C, W, TH);
   const int DS = twd_ds(TH, W), XF = C * G.PS;  // dy planes start at float XF
+  __shared__ float bnf[2][20];
+  if (a.fm) {
+    if (tid < C) {
+      bnf[0][tid] = a.fm[tid];
+      bnf[1][tid] = a.fi[tid];
+    }
+    __syncthreads();
+  }
   int joff[NJ];
 #pragma unroll
   for (int n = 0; n < NJ; ++n) {
@@ -1090,6 +1187,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
     float* cur = (it & 1) ? buf1 : buf0;
     float* nxt = (it & 1) ? buf0 : buf1;
     td_wait_vm0();
+    if (a.fm) twd_bn_fold(stg, a, H, d, tile, cur, bnf, wave, lane, G.PS);
     __syncthreads();
     if (tile + (int)gridDim.x < ntile) issue(tile + gridDim.x, nxt);
     const int b = tile / a.g.nband;
@@ -1234,6 +1332,14 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3q_kernel(WgradArgs a) {
     for (int h = 0; h < NH; ++h) acc[g][h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int n = 0; n < (HY ? NJ : 1); ++n) acc16[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  __shared__ float bnf[2][20];
+  if (a.fm) {
+    if (tid < C) {
+      bnf[0][tid] = a.fm[tid];
+      bnf[1][tid] = a.fi[tid];
+    }
+    __syncthreads();
+  }
   TwdStage stg;
   twd_stage_init(stg, C, H, W, TH, G, wave, lane);
   const int ntile = a.B * a.g.nband;
@@ -1248,6 +1354,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3q_kernel(WgradArgs a) {
     float* cur = (it & 1) ? buf1 : buf0;
     float* nxt = (it & 1) ? buf0 : buf1;
     td_wait_vm0();
+    if (a.fm) twd_bn_fold(stg, a, H, d, tile, cur, bnf, wave, lane, G.PS);  // x: the layer below's s -> y
     __syncthreads();
     if (tile + (int)gridDim.x < ntile) twd_issue(stg, a, C, H, W, d, tile + gridDim.x, nxt, wave);
     const int b = tile / a.g.nband;
@@ -1670,12 +1777,15 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const float* __restrict__
 
 // g = v[c] (gy - u[c] - y w[c]) [+ gs]; gold (may be null) = g; gh = h > 0 ? g : 0
 // (MASK: the conv epilogue's bit mask in place of h: word [b][p], bit c = !(h <= 0))
-template <bool MASK>
+// (FOLD: y holds the tail's s, the BatchNorm output is (s - ym[c]) v[c] -- tail_fwd_kernel's
+// expression; the tail wrote no y, its next conv folded it in)
+template <bool MASK, bool FOLD = false>
 __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ y,
                                                        const float* __restrict__ gs, const void* __restrict__ hm,
                                                        const float* __restrict__ u, const float* __restrict__ v,
                                                        const float* __restrict__ w, float* __restrict__ gh,
-                                                       float* __restrict__ gold, int64_t total, int C, int HW) {
+                                                       float* __restrict__ gold, int64_t total, int C, int HW,
+                                                       const float* __restrict__ ym) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float* h = (const float*)hm;
   const unsigned* mk = (const unsigned*)hm;
@@ -1684,7 +1794,9 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__
     if (i4 >= total) return;
     const int64_t bc = i4 / HW;
     const int c = (int)(bc % C);
-    const float4 av = *(const float4*)(gy + i4), bv = *(const float4*)(y + i4);
+    const float4 av = *(const float4*)(gy + i4);
+    float4 bv = *(const float4*)(y + i4);
+    if constexpr (FOLD) bv = float4{(bv.x - ym[c]) * v[c], (bv.y - ym[c]) * v[c], (bv.z - ym[c]) * v[c], (bv.w - ym[c]) * v[c]};
     float4 hv;
     if constexpr (MASK) {
       // the 4 pixels' words (pixel p = i4 - bc HW of clip b = bc / C)
@@ -1708,7 +1820,8 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(const float* __restrict__
   if (i >= total) return;
   const int64_t bc = i / HW;
   const int c = (int)(bc % C);
-  float g = v[c] * (gy[i] - u[c] - y[i] * w[c]);
+  const float yv = FOLD ? (y[i] - ym[c]) * v[c] : y[i];
+  float g = v[c] * (gy[i] - u[c] - yv * w[c]);
   if (gs) g = g + gs[i];
   if (gold) gold[i] = g;
   if constexpr (MASK) gh[i] = ((mk[(bc / C) * HW + (i - bc * HW)] >> c) & 1u) ? g : 0.f;
@@ -2093,9 +2206,9 @@ extern "C" size_t honk_conv3x3_wgrad_workspace_bytes(int64_t batch, int32_t c, i
   return (size_t)train::tc_grid(t) * c * c * 9 * sizeof(float);
 }
 
-extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
-                                      int32_t h, int32_t w_, int32_t dil, void* workspace, size_t ws_bytes,
-                                      void* stream) {
+namespace {
+int conv3x3_wgrad(const float* x, const float* dy, float* dw, int64_t batch, int32_t c, int32_t h, int32_t w_,
+                  int32_t dil, const float* fm, const float* fi, void* workspace, size_t ws_bytes, void* stream) {
   int rc = tc_check(x, dy, dw, batch, c, h, w_, dil);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
@@ -2109,7 +2222,9 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
   train::WgradArgs a;
   a.x = x; a.dy = dy; a.part = (float*)workspace;
   a.B = (int)batch; a.H = h; a.W = w_;
+  a.fm = fm; a.fi = fi;
   const WgradPlan wp = wgrad_plan(batch, c, h, w_, dil);
+  if (fm && !wp.dma) return fail(HONK_ERR_UNSUPPORTED, "conv3x3 wgrad: folded BatchNorm needs the DMA-staged kernels");
   a.g = wp.g;
   const int grid = wp.grid;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
@@ -2134,6 +2249,20 @@ extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw
                      n, grid);
   HONK_LAUNCH_CHECK("wsum_kernel");
   return HONK_OK;
+}
+}  // namespace
+
+extern "C" int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
+                                      int32_t h, int32_t w_, int32_t dil, void* workspace, size_t ws_bytes,
+                                      void* stream) {
+  return conv3x3_wgrad(x, dy, dw, batch, c, h, w_, dil, nullptr, nullptr, workspace, ws_bytes, stream);
+}
+
+extern "C" int honk_conv3x3_wgrad_bn_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c,
+                                         int32_t h, int32_t w_, int32_t dil, const float* fold_mean,
+                                         const float* fold_invstd, void* workspace, size_t ws_bytes, void* stream) {
+  if (!fold_mean || !fold_invstd) return fail(HONK_ERR_ARG, "null pointer argument");
+  return conv3x3_wgrad(x, dy, dw, batch, c, h, w_, dil, fold_mean, fold_invstd, workspace, ws_bytes, stream);
 }
 
 extern "C" size_t honk_bn_train_workspace_bytes(int64_t batch, int32_t c, int64_t hw) {
@@ -2231,7 +2360,8 @@ extern "C" int honk_res_tail_bwd_f32(const float* gy, const float* gs, const flo
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
   hipLaunchKernelGGL(train::tail_bwd_kernel<false>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
-                     (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
+                     (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw,
+                     (const float*)nullptr);
   HONK_LAUNCH_CHECK("tail_bwd_kernel");
   return HONK_OK;
 }
@@ -2249,14 +2379,32 @@ int stats_grid(int64_t batch, int c, int h, int w_, int dil) {
 }
 }  // namespace
 
+namespace {
+// conv3x3d_kernel with the statistics epilogue: mode 1 / 2, the fixed-geometry instance
+// where it applies, the folded-BatchNorm instance when a.fm is set
+void launch_conv_stats(const train::Conv3Args& a, int mode, int S, hipStream_t st) {
+  const bool fx = train::td_fixed(a), fo = a.fm != nullptr;
+#define HONK_CS(M, FO)                                                                                           \
+  if (fx) hipLaunchKernelGGL((train::conv3x3d_kernel<19, M, 20, 1, 25, FO>), dim3(S), dim3(512), 0, st, a); \
+  else hipLaunchKernelGGL((train::conv3x3d_kernel<19, M, 0, 0, 0, FO>), dim3(S), dim3(512), 0, st, a);
+  if (mode == 1 && fo) { HONK_CS(1, true) }
+  else if (mode == 1) { HONK_CS(1, false) }
+  else if (fo) { HONK_CS(2, true) }
+  else { HONK_CS(2, false) }
+#undef HONK_CS
+}
+}  // namespace
+
 extern "C" size_t honk_conv3x3_stats_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil) {
   const int S = stats_grid(batch, c, h, w_, dil);
   return S > 0 ? (size_t)c * S * 2 * sizeof(double) + (size_t)4 * c * sizeof(float) : 0;
 }
 
-extern "C" int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
-                                      int32_t w_, int32_t dil, int32_t flip, int32_t mode, const float* aux,
-                                      void* stats, size_t stats_bytes, void* stream) {
+extern "C" int honk_conv3x3_stats_bn_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c,
+                                         int32_t h, int32_t w_, int32_t dil, int32_t flip, int32_t mode,
+                                         const float* aux, const float* fold_mean, const float* fold_invstd,
+                                         void* stats, size_t stats_bytes, void* stream) {
+  if (!fold_mean != !fold_invstd) return fail(HONK_ERR_ARG, "null pointer argument");
   int rc = tc_check(x, w, y, batch, c, h, w_, dil);
   if (rc) return rc;
   if (mode != 1 && mode != 2) return fail(HONK_ERR_ARG, "conv3x3 statistics mode %d (1 or 2)", mode);
@@ -2273,24 +2421,27 @@ extern "C" int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, 
   a.aux = aux;
   a.part = (double*)stats;
   a.mask = nullptr;
+  a.fm = fold_mean; a.fi = fold_invstd;
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (train::td_fixed(a)) {
-    if (mode == 1) hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1, 20, 1, 25>), dim3(S), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((train::conv3x3d_kernel<19, 2, 20, 1, 25>), dim3(S), dim3(512), 0, st, a);
-  } else if (mode == 1) {
-    hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
-  } else {
-    hipLaunchKernelGGL((train::conv3x3d_kernel<19, 2>), dim3(S), dim3(512), 0, st, a);
-  }
+  launch_conv_stats(a, mode, S, st);
   tl.done(st);
   HONK_LAUNCH_CHECK("conv3x3d_kernel");
   return HONK_OK;
 }
 
-extern "C" int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, uint32_t* mask, int64_t batch,
-                                     int32_t c, int32_t h, int32_t w_, int32_t dil, const float* old, void* stats,
-                                     size_t stats_bytes, void* stream) {
+extern "C" int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
+                                      int32_t w_, int32_t dil, int32_t flip, int32_t mode, const float* aux,
+                                      void* stats, size_t stats_bytes, void* stream) {
+  return honk_conv3x3_stats_bn_f32(x, w, y, batch, c, h, w_, dil, flip, mode, aux, nullptr, nullptr, stats,
+                                   stats_bytes, stream);
+}
+
+extern "C" int honk_conv3x3_tail_bn_f32(const float* x, const float* w, float* s, uint32_t* mask, int64_t batch,
+                                        int32_t c, int32_t h, int32_t w_, int32_t dil, const float* old,
+                                        const float* fold_mean, const float* fold_invstd, void* stats,
+                                        size_t stats_bytes, void* stream) {
+  if (!fold_mean != !fold_invstd) return fail(HONK_ERR_ARG, "null pointer argument");
   int rc = tc_check(x, w, s, batch, c, h, w_, dil);
   if (rc) return rc;
   if (!mask) return fail(HONK_ERR_ARG, "null pointer argument");
@@ -2306,19 +2457,32 @@ extern "C" int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, u
   a.aux = old;
   a.part = (double*)stats;
   a.mask = mask;
+  a.fm = fold_mean; a.fi = fold_invstd;
   hipStream_t st = (hipStream_t)stream;
   TimedLaunch tl(st, 2.0 * (double)batch * h * w_ * c * c * 9);
-  if (train::td_fixed(a)) hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1, 20, 1, 25>), dim3(S), dim3(512), 0, st, a);
-  else hipLaunchKernelGGL((train::conv3x3d_kernel<19, 1>), dim3(S), dim3(512), 0, st, a);
+  launch_conv_stats(a, 1, S, st);
   tl.done(st);
   HONK_LAUNCH_CHECK("conv3x3d_kernel (tail epilogue)");
+  return HONK_OK;
+}
+
+extern "C" int honk_conv3x3_tail_f32(const float* x, const float* w, float* s, uint32_t* mask, int64_t batch,
+                                     int32_t c, int32_t h, int32_t w_, int32_t dil, const float* old, void* stats,
+                                     size_t stats_bytes, void* stream) {
+  return honk_conv3x3_tail_bn_f32(x, w, s, mask, batch, c, h, w_, dil, old, nullptr, nullptr, stats, stats_bytes,
+                                  stream);
+}
+
+extern "C" int honk_conv3x3_bn_fold_check(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil) {
+  if (stats_grid(batch, c, h, w_, dil) <= 0 || !wgrad_plan(batch, c, h, w_, dil).dma)
+    return fail(HONK_ERR_UNSUPPORTED, "conv3x3: no folded BatchNorm for this shape");
   return HONK_OK;
 }
 
 extern "C" int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, float* invstd, float* running_mean,
                                        float* running_var, const void* stats, int64_t batch, int32_t c, int32_t hh,
                                        int32_t ww, int32_t dil, float momentum, float eps, void* stream) {
-  if (!s || !y || !mean || !invstd || !stats || (!running_mean != !running_var))
+  if (!s || !mean || !invstd || !stats || (!running_mean != !running_var))
     return fail(HONK_ERR_ARG, "null pointer argument");
   const int S = stats_grid(batch, c, hh, ww, dil);
   if (S <= 0) return fail(HONK_ERR_UNSUPPORTED, "res tail: no statistics epilogue for this shape");
@@ -2327,6 +2491,7 @@ extern "C" int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, fl
   hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)stats,
                      mean, invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
   HONK_LAUNCH_CHECK("bn_stats_kernel");
+  if (!y) return HONK_OK;  // the next conv folds the BatchNorm in (honk_conv3x3_tail_bn_f32)
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
   hipLaunchKernelGGL(train::tail_fwd_kernel<true>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, s,
@@ -2336,11 +2501,12 @@ extern "C" int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, fl
   return HONK_OK;
 }
 
-extern "C" int honk_res_tail_bwd_mask_f32(const float* gy, const float* gs, const float* y, const float* invstd,
-                                          const uint32_t* mask, float* gh, float* gold, int64_t batch, int32_t c,
-                                          int32_t hh, int32_t ww, int32_t dil, void* stats, size_t stats_bytes,
-                                          void* stream) {
+namespace {
+int res_tail_bwd_mask(const float* gy, const float* gs, const float* y, const float* ym, const float* invstd,
+                      const uint32_t* mask, float* gh, float* gold, int64_t batch, int32_t c, int32_t hh, int32_t ww,
+                      int32_t dil, void* stats, size_t stats_bytes, void* stream) {
   if (!gy || !y || !invstd || !mask || !gh || !stats) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (ym && dil <= 0) return fail(HONK_ERR_UNSUPPORTED, "res tail: a folded BatchNorm needs the conv's statistics");
   if (batch < 1 || c < 1 || hh < 1 || ww < 1 || batch > 0x7fffffff || (int64_t)hh * ww > 0x7fffffff)
     return fail(HONK_ERR_ARG, "bad res tail shape");
   hipStream_t st = (hipStream_t)stream;
@@ -2367,10 +2533,34 @@ extern "C" int honk_res_tail_bwd_mask_f32(const float* gy, const float* gs, cons
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
-  hipLaunchKernelGGL(train::tail_bwd_kernel<true>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs,
-                     (const void*)mask, (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
+  if (ym)
+    hipLaunchKernelGGL((train::tail_bwd_kernel<true, true>), dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y,
+                       gs, (const void*)mask, (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c,
+                       (int)hw, ym);
+  else
+    hipLaunchKernelGGL((train::tail_bwd_kernel<true>), dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs,
+                       (const void*)mask, (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw,
+                       (const float*)nullptr);
   HONK_LAUNCH_CHECK("tail_bwd_kernel");
   return HONK_OK;
+}
+}  // namespace
+
+extern "C" int honk_res_tail_bwd_mask_f32(const float* gy, const float* gs, const float* y, const float* invstd,
+                                          const uint32_t* mask, float* gh, float* gold, int64_t batch, int32_t c,
+                                          int32_t hh, int32_t ww, int32_t dil, void* stats, size_t stats_bytes,
+                                          void* stream) {
+  return res_tail_bwd_mask(gy, gs, y, nullptr, invstd, mask, gh, gold, batch, c, hh, ww, dil, stats, stats_bytes,
+                           stream);
+}
+
+extern "C" int honk_res_tail_bwd_mask_bn_f32(const float* gy, const float* gs, const float* s, const float* mean,
+                                             const float* invstd, const uint32_t* mask, float* gh, float* gold,
+                                             int64_t batch, int32_t c, int32_t hh, int32_t ww, int32_t dil,
+                                             void* stats, size_t stats_bytes, void* stream) {
+  if (!mean) return fail(HONK_ERR_ARG, "null pointer argument");
+  return res_tail_bwd_mask(gy, gs, s, mean, invstd, mask, gh, gold, batch, c, hh, ww, dil, stats, stats_bytes,
+                           stream);
 }
 
 extern "C" int honk_res_tail_fwd_part_f32(const float* h, const float* old, float* s, float* y, float* mean,
@@ -2410,7 +2600,8 @@ extern "C" int honk_res_tail_bwd_part_f32(const float* gy, const float* gs, cons
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
   hipLaunchKernelGGL(train::tail_bwd_kernel<false>, dim3((unsigned)cdiv(nthr, 256)), dim3(256), 0, st, gy, y, gs, h,
-                     (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw);
+                     (const float*)m, invstd, (const float*)(m + c), gh, gold, total, c, (int)hw,
+                     (const float*)nullptr);
   HONK_LAUNCH_CHECK("tail_bwd_kernel");
   return HONK_OK;
 }

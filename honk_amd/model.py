@@ -190,12 +190,18 @@ class SpeechResModel(SerializableModule):
                 old = old_x if i % 2 == 0 else None
                 h = _conv3x3.conv3x3(x, conv.weight, d, old=old, box_out=box, box_in=box_in)
                 bn = getattr(self, "bn{}".format(i))
+                # the BatchNorm goes into the next block's conv when that conv takes it
+                # (the last block's output feeds the head: materialized)
+                nxt = getattr(self, "conv{}".format(i + 1), None) if i < self.n_layers else None
+                fold = nxt is not None and _conv3x3.supported(h, nxt) and \
+                    _conv3x3.bn_supported(h, getattr(self, "bn{}".format(i + 1))) and \
+                    _conv3x3.fold_supported(h, nxt.dilation[0])
                 if i % 2 == 0:
                     keep = i + 2 <= self.n_layers  # old_x is read again by layer i + 2
-                    out = _conv3x3.res_tail(h, old_x, bn, keep_s=keep, box=box)
+                    out = _conv3x3.res_tail(h, old_x, bn, keep_s=keep, box=box, fold=fold)
                     x, old_x = out if keep else (out, None)
                 else:
-                    x = _conv3x3.res_tail(h, None, bn, box=box)
+                    x = _conv3x3.res_tail(h, None, bn, box=box, fold=fold)
                 box_in = box
                 continue
             box_in = None

@@ -293,6 +293,38 @@ size_t honk_conv3x3_stats_bytes(int64_t batch, int32_t c, int32_t h, int32_t w_,
 int honk_conv3x3_stats_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
                            int32_t w_, int32_t dil, int32_t flip, int32_t mode, const float* aux, void* stats,
                            size_t stats_bytes, void* stream);
+/*
+ * The train BatchNorm of a res block folded into the next conv (res26-narrow's C5 step:
+ * one HBM pass less per block -- the tail writes no y).  honk_res_tail_fwd_s_f32 with
+ * y = NULL computes only mean / invstd / the running statistics; the consumers of y then
+ * take that block's s with its (fold_mean, fold_invstd) and make y = (s - mean) * invstd
+ * where they read it, tail_fwd's fp32 expression (bit-identical to the materialized y):
+ *   honk_conv3x3_tail_bn_f32 / honk_conv3x3_stats_bn_f32 mode 1 -- the forward conv's
+ *   input x (its staged tile, in LDS; the conv's zero padding stays zero);
+ *   honk_conv3x3_stats_bn_f32 mode 2 -- the input-gradient conv's aux;
+ *   honk_conv3x3_wgrad_bn_f32 -- the weight-gradient conv's x;
+ *   honk_res_tail_bwd_mask_bn_f32 -- the tail backward's y (s = that tail's s, mean its
+ *   mean; dil >= 1 only: a folded block always feeds an input-gradient conv).
+ * The NULL-fold forms are the entry points above.  honk_conv3x3_bn_fold_check: HONK_OK when
+ * the shape has all four (the statistics epilogue's shapes whose weight gradient runs on
+ * the LDS-DMA kernels).  Replaces no reference call: the reference's bn (model.py:117-118)
+ * is one module the drop-in keeps; this is the same arithmetic in a different kernel.
+ */
+int honk_conv3x3_bn_fold_check(int64_t batch, int32_t c, int32_t h, int32_t w_, int32_t dil);
+int honk_conv3x3_tail_bn_f32(const float* x, const float* w, float* s, uint32_t* mask, int64_t batch, int32_t c,
+                             int32_t h, int32_t w_, int32_t dil, const float* old, const float* fold_mean,
+                             const float* fold_invstd, void* stats, size_t stats_bytes, void* stream);
+int honk_conv3x3_stats_bn_f32(const float* x, const float* w, float* y, int64_t batch, int32_t c, int32_t h,
+                              int32_t w_, int32_t dil, int32_t flip, int32_t mode, const float* aux,
+                              const float* fold_mean, const float* fold_invstd, void* stats, size_t stats_bytes,
+                              void* stream);
+int honk_conv3x3_wgrad_bn_f32(const float* x, const float* dy, float* dw, int64_t batch, int32_t c, int32_t h,
+                              int32_t w_, int32_t dil, const float* fold_mean, const float* fold_invstd,
+                              void* workspace, size_t ws_bytes, void* stream);
+int honk_res_tail_bwd_mask_bn_f32(const float* gy, const float* gs, const float* s, const float* mean,
+                                  const float* invstd, const uint32_t* mask, float* gh, float* gold, int64_t batch,
+                                  int32_t c, int32_t hh, int32_t ww, int32_t dil, void* stats, size_t stats_bytes,
+                                  void* stream);
 int honk_res_tail_fwd_part_f32(const float* h, const float* old, float* s, float* y, float* mean, float* invstd,
                                float* running_mean, float* running_var, const void* stats, int64_t batch, int32_t c,
                                int32_t h_, int32_t w_, int32_t dil, float momentum, float eps, void* stream);

@@ -412,3 +412,45 @@ def test_fused_tail_statistics_large_mean(keep):
     print(f"keep={keep}: running_var rel err {rv:.2e} (var ~ {float(var.mean()):.2e})")
     assert rv < 1e-3
     del out
+
+
+@pytest.mark.parametrize("name,n_layers,B,env", [
+    ("res26-narrow", 6, 48, None), ("res15-narrow", 13, 6, None), ("res26-narrow", 5, 9, None),
+    ("res26-narrow", 4, 40, ("HONK_WGRAD", "d")), ("res26-narrow", 4, 40, ("HONK_TD_FIXED", "0"))])
+def test_folded_bn_step_bitwise(monkeypatch, name, n_layers, B, env):
+    """Each block's train BatchNorm folded into the next block's conv (the tail writes no y:
+    honk_res_tail_fwd_s_f32 with y = NULL, then honk_conv3x3_tail_bn_f32 / _stats_bn_f32
+    mode 2 / _wgrad_bn_f32 / honk_res_tail_bwd_mask_bn_f32 make y = (s - mean) * invstd
+    where they read it) vs the materialized y: one training step, bit-identical loss,
+    gradients and running statistics; every block whose conv and next conv are on the
+    LDS-DMA kernels folds (res15-narrow: dilation <= 4, blocks 1..8 of 13), the last
+    block's output stays materialized for the head.  Also under the d wgrad kernel and
+    the runtime-geometry instances."""
+    if env is not None:
+        monkeypatch.setenv(*env)
+    cfg = dict(hm.find_config(name))
+    cfg["n_layers"] = n_layers
+    dil = [2 ** ((i - 1) // 3) if cfg.get("use_dilation") else 1 for i in range(1, n_layers + 1)]  # model.py:93-98
+    want = sum(dil[i] <= 4 and dil[i + 1] <= 4 for i in range(n_layers - 1))
+
+    def step(fold):
+        monkeypatch.setattr(hc, "FOLD_BN", fold)
+        torch.manual_seed(3)
+        m = hm.find_model(name)(cfg).to(DEV).train()
+        g = torch.Generator(device=DEV).manual_seed(6)
+        x = torch.randn(B, 101, 40, device=DEV, generator=g)
+        y = torch.randint(0, 12, (B,), device=DEV, generator=g)
+        n0 = hc.FOLD_USED["n"]
+        loss = torch.nn.functional.cross_entropy(m(x), y)
+        loss.backward()
+        bufs = {k: b.clone() for k, b in m.named_buffers()}
+        return loss.detach(), {k: p.grad.clone() for k, p in m.named_parameters()}, bufs, hc.FOLD_USED["n"] - n0
+
+    l1, g1, b1, n1 = step(True)
+    l2, g2, b2, n2 = step(False)
+    assert (n1, n2) == (want, 0)
+    assert torch.equal(l1, l2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+    for k in b1:
+        assert torch.equal(b1[k], b2[k]), k
