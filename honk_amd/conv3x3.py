@@ -161,7 +161,7 @@ def _wgrad_fold(xs, dy, d, fold):
 FUSE_TAIL = os.environ.get("HONK_TRAIN_FUSE_TAIL", "1") != "0"   # tests compare both
 # a block's train BatchNorm folded into the next conv (its forward, input-gradient and
 # weight-gradient kernels make y from s where they read it; the tail writes no y)
-FOLD_BN = os.environ.get("HONK_TRAIN_FOLD_BN", "0") == "1"
+FOLD_BN = os.environ.get("HONK_TRAIN_FOLD_BN", "1") != "0"
 
 
 def fold_supported(h, d_next) -> bool:

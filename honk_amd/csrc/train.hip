@@ -416,25 +416,22 @@ __host__ __device__ inline TdGeo td_geo(int C, int W, int TH) {
 
 // The folded BatchNorm on a staged tile (conv3x3d_kernel MODE 1, wgrad3x3d/q_kernel):
 // each lane rewrites the 16-B chunks its own LDS-DMA instructions wrote (chunk e = base_e
-// + 64 i at float 4 e; plane c = 4 e / PS), right after its own vmcnt wait and before the
-// tile's barrier -- no barrier of its own.  An in-image x chunk (ok[i]) holds the layer
-// below's s and becomes (s - mean[c]) invstd[c], tail_fwd_kernel's fp32 expression
-// (bit-identical to the y it would have written); pad columns and out-of-image rows stay
-// zero (the conv's zero padding of y).  bnf: mean in [0][c], invstd in [1][c] (LDS).
+// + 64 i at float 4 e, of plane c = 4 e / PS: the mapping is tile-invariant), right after
+// its own vmcnt wait and before the tile's barrier -- no barrier of its own.  An in-image x
+// chunk (ok[i]) holds the layer below's s and becomes (s - mean[c]) invstd[c] (mv[i] =
+// {mean, invstd} of its plane), tail_fwd_kernel's fp32 expression: bit-identical to the y
+// it would have written; pad columns and out-of-image rows stay zero (the conv's zero
+// padding of y).
 template <int N>
-__device__ __forceinline__ void td_bn_fold(float* buf, const float (*bnf)[20], int base_e, int PS,
-                                           const bool (&ok)[N]) {
+__device__ __forceinline__ void td_bn_fold(float* buf, int base_e, const bool (&ok)[N], const float2 (&mv)[N]) {
   float4 v[N];
-  int c[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    c[i] = 4 * (base_e + 64 * i) / PS;
+  for (int i = 0; i < N; ++i)
     if (ok[i]) v[i] = *(const float4*)(buf + 4 * (base_e + 64 * i));
-  }
 #pragma unroll
   for (int i = 0; i < N; ++i)
     if (ok[i]) {
-      const float m = bnf[0][c[i]], iv = bnf[1][c[i]];
+      const float m = mv[i].x, iv = mv[i].y;
       *(float4*)(buf + 4 * (base_e + 64 * i)) =
           float4{(v[i].x - m) * iv, (v[i].y - m) * iv, (v[i].z - m) * iv, (v[i].w - m) * iv};
     }
@@ -503,7 +500,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
   static_assert(C <= 20, "conv3x3d_kernel: C <= 20");
   constexpr int K = 9 * C, KT = (K + 15) / 16, NG = (C + 3) / 4, PF = 8;  // PF: reads in flight
   __shared__ __attribute__((aligned(16))) float tdl[2 * TD_BUF / 4];
-  __shared__ float bnf[2][20];  // the folded BatchNorm's mean / invstd (a.fm)
+  __shared__ float2 bnf[20];  // the folded BatchNorm's {mean, invstd} per channel (a.fm)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr bool FIX = FW > 0 && FD > 0 && FTH > 0;
@@ -514,10 +511,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
   // memory operation among the k loop's counted LDS reads)
   float fmv = 0.f, fiv = 0.f;
   if (fold) {
-    if (MODE == 1 && tid < C) {
-      bnf[0][tid] = a.fm[tid];
-      bnf[1][tid] = a.fi[tid];
-    }
+    if (MODE == 1 && tid < C) bnf[tid] = float2{a.fm[tid], a.fi[tid]};
     if (MODE == 2 && lane < C) {
       fmv = a.fm[lane];
       fiv = a.fi[lane];
@@ -650,12 +644,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3d_kernel(Conv3Args a) {
       band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
       const int hr = r + (k0 - 1) * d;
       bool ok[TD_ITER];
+      float2 mv[TD_ITER];
 #pragma unroll
       for (int i = 0; i < TD_ITER; ++i) {
         const int h = hr + crow[i] * d;
         ok[i] = cbase[i] >= 0 && h >= 0 && h < H;
+        mv[i] = ok[i] ? bnf[4 * ((wave * TD_ITER + i) * 64 + lane) / PS] : float2{0.f, 0.f};
       }
-      td_bn_fold(cur, bnf, wave * TD_ITER * 64 + lane, PS, ok);
+      td_bn_fold(cur, wave * TD_ITER * 64 + lane, ok, mv);
     }
     __syncthreads();  // this tile's DMA landed everywhere; nobody reads nxt any more
     if (tile + (int)gridDim.x < ntile) issue(tile + gridDim.x, nxt);
@@ -1125,7 +1121,7 @@ __device__ __forceinline__ void twd_issue(const TwdStage& s, const WgradArgs& a,
 
 // td_bn_fold on this lane's x chunks of tile `tile` (kind 1, in-image rows)
 __device__ __forceinline__ void twd_bn_fold(const TwdStage& s, const WgradArgs& a, int H, int d, int tile, float* buf,
-                                            const float (*bnf)[20], int wave, int lane, int PS) {
+                                            const float2 (&mv)[TWD_ITER], int wave, int lane) {
   const int b = tile / a.g.nband;
   int r, k0, th;
   band_of(a.g, H, tile - b * a.g.nband, r, k0, th);
@@ -1136,7 +1132,16 @@ __device__ __forceinline__ void twd_bn_fold(const TwdStage& s, const WgradArgs& 
     const int h = hb + s.crow[i] * d;
     ok[i] = s.ckind[i] == 1 && h >= 0 && h < H;
   }
-  td_bn_fold(buf, bnf, wave * TWD_ITER * 64 + lane, PS, ok);
+  td_bn_fold(buf, wave * TWD_ITER * 64 + lane, ok, mv);
+}
+// the {mean, invstd} of this lane's x chunks' planes (tile-invariant), {0, 0} elsewhere
+__device__ __forceinline__ void twd_bn_mv(float2 (&mv)[TWD_ITER], const TwdStage& s, const WgradArgs& a, int wave,
+                                         int lane, int PS) {
+#pragma unroll
+  for (int i = 0; i < TWD_ITER; ++i) {
+    const int c = 4 * ((wave * TWD_ITER + i) * 64 + lane) / PS;
+    mv[i] = s.ckind[i] == 1 ? float2{a.fm[c], a.fi[c]} : float2{0.f, 0.f};
+  }
 }
 
 // FW, FD, FTH (all > 0): compile-time tile geometry, as conv3x3d_kernel's
@@ -1152,14 +1157,6 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   const int d = FIX ? FD : a.g.d, W = FIX ? FW : a.W, H = a.H, TH = FIX ? FTH : a.g.TH;
   const TdGeo G = td_geo(C, W, TH);
   const int DS = twd_ds(TH, W), XF = C * G.PS;  // dy planes start at float XF
-  __shared__ float bnf[2][20];
-  if (a.fm) {
-    if (tid < C) {
-      bnf[0][tid] = a.fm[tid];
-      bnf[1][tid] = a.fi[tid];
-    }
-    __syncthreads();
-  }
   int joff[NJ];
 #pragma unroll
   for (int n = 0; n < NJ; ++n) {
@@ -1176,6 +1173,8 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
   for (int h = 0; h < NH; ++h) acc4[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   TwdStage stg;
   twd_stage_init(stg, C, H, W, TH, G, wave, lane);
+  float2 fmv[TWD_ITER];
+  if (a.fm) twd_bn_mv(fmv, stg, a, wave, lane, G.PS);
   const int ntile = a.B * a.g.nband;
   auto issue = [&](int tile, float* buf) { twd_issue(stg, a, C, H, W, d, tile, buf, wave); };
   float* buf0 = tdl;
@@ -1187,7 +1186,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3d_kernel(WgradArgs a) {
     float* cur = (it & 1) ? buf1 : buf0;
     float* nxt = (it & 1) ? buf0 : buf1;
     td_wait_vm0();
-    if (a.fm) twd_bn_fold(stg, a, H, d, tile, cur, bnf, wave, lane, G.PS);
+    if (a.fm) twd_bn_fold(stg, a, H, d, tile, cur, fmv, wave, lane);
     __syncthreads();
     if (tile + (int)gridDim.x < ntile) issue(tile + gridDim.x, nxt);
     const int b = tile / a.g.nband;
@@ -1332,16 +1331,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3q_kernel(WgradArgs a) {
     for (int h = 0; h < NH; ++h) acc[g][h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int n = 0; n < (HY ? NJ : 1); ++n) acc16[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  __shared__ float bnf[2][20];
-  if (a.fm) {
-    if (tid < C) {
-      bnf[0][tid] = a.fm[tid];
-      bnf[1][tid] = a.fi[tid];
-    }
-    __syncthreads();
-  }
   TwdStage stg;
   twd_stage_init(stg, C, H, W, TH, G, wave, lane);
+  float2 fmv[TWD_ITER];
+  if (a.fm) twd_bn_mv(fmv, stg, a, wave, lane, G.PS);
   const int ntile = a.B * a.g.nband;
   float* buf0 = tdl;
   float* buf1 = tdl + TWD_BUF / 4;
@@ -1354,7 +1347,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3q_kernel(WgradArgs a) {
     float* cur = (it & 1) ? buf1 : buf0;
     float* nxt = (it & 1) ? buf0 : buf1;
     td_wait_vm0();
-    if (a.fm) twd_bn_fold(stg, a, H, d, tile, cur, bnf, wave, lane, G.PS);  // x: the layer below's s -> y
+    if (a.fm) twd_bn_fold(stg, a, H, d, tile, cur, fmv, wave, lane);  // x: the layer below's s -> y
     __syncthreads();
     if (tile + (int)gridDim.x < ntile) twd_issue(stg, a, C, H, W, d, tile + gridDim.x, nxt, wave);
     const int b = tile / a.g.nband;
