@@ -23,6 +23,11 @@ class ResDesc(ctypes.Structure):
 
 
 PRECISIONS = {"f32": 0, "bf16": 1, "bf16x3": 2, "f16x2": 3}
+PREC_AUTO = 4  # HONK_PREC_AUTO: honk_res_select_precision's "fastest mode holding 1e-4"
+PRECISION_NAMES = {v: k for k, v in PRECISIONS.items()}
+NUM_COUNT = 8  # HONK_NUM_COUNT
+NUM_FIELDS = ("scale", "range", "w0sum", "rho", "f16_overflow", "rho_layer", "valid", "out_scale")  # HONK_NUM_*
+NUM_KW = 64  # HONK_NUM_KW: the per-layer f16x2 weight exponents follow the header
 
 
 class CnnDesc(ctypes.Structure):
@@ -42,6 +47,10 @@ _PROTOS = {
                                             ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     "honk_res_pack": (ctypes.c_int, [ctypes.POINTER(ResDesc), ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32,
                                      c_f32p, ctypes.c_void_p]),
+    "honk_res_numerics": (ctypes.c_int, [ctypes.POINTER(ResDesc), c_f32p, ctypes.POINTER(ctypes.c_float),
+                                         ctypes.c_int32, ctypes.c_void_p]),
+    "honk_res_select_precision": (ctypes.c_int, [ctypes.POINTER(ResDesc), ctypes.POINTER(ctypes.c_float),
+                                                 ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]),
     "honk_res_forward": (ctypes.c_int, [ctypes.POINTER(ResDesc), c_f32p, c_f32p, c_f32p, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "honk_cnn_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(CnnDesc), ctypes.c_int64]),
@@ -215,3 +224,26 @@ def res_launch_plan(desc, batch: int, n_cus: int = 0):
     if n < 0:
         check(n, "honk_res_launch_plan")
     return [KERNEL_NAMES[kinds[i]] for i in range(min(n, 256))]
+
+
+def res_numerics(desc, packed, device):
+    """The pack-time numerics record of a packed res model (HONK_NUM_*) as a dict;
+    synchronises the device's current stream (once per pack)."""
+    n = NUM_KW + desc.n_layers
+    rec = (ctypes.c_float * n)()
+    check(load().honk_res_numerics(ctypes.byref(desc), packed.data_ptr(), rec, n, stream_handle(device)),
+          "honk_res_numerics")
+    out = {k: float(rec[i]) for i, k in enumerate(NUM_FIELDS)}
+    out["kw"] = [int(rec[NUM_KW + i]) for i in range(desc.n_layers)]
+    return out, rec
+
+
+def res_select_precision(desc, rec, requested: str):
+    """honk_res_select_precision: (precision name to run, note on why the request was
+    not taken or "")."""
+    note = ctypes.create_string_buffer(512)
+    req = PREC_AUTO if requested == "auto" else PRECISIONS[requested]
+    p = load().honk_res_select_precision(ctypes.byref(desc), rec, req, note, len(note))
+    if p < 0:
+        check(p, "honk_res_select_precision")
+    return PRECISION_NAMES[p], note.value.decode(errors="replace")

@@ -39,13 +39,19 @@ def build(force=False, verbose=False):
     base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
             "-I", os.path.join(HERE, "..", "include")]
     procs = []
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))] + [
+        os.path.join(HERE, "..", "include", "honk_hip.h")]
     for src in SOURCES:
         obj = os.path.join(tmp, src.rsplit(".", 1)[0] + ".o")
+        objs.append(obj)
+        # incremental: an object newer than its source and every shared header is kept
+        if not force and os.path.exists(obj) and all(
+                os.path.getmtime(obj) > os.path.getmtime(p) for p in [os.path.join(CSRC, src)] + headers):
+            continue
         cmd = base + (["-x", "hip"] if src.endswith(".cpp") else []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
-        objs.append(obj)
     for src, p in procs:
         out, _ = p.communicate()
         if p.returncode != 0:

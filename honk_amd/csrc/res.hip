@@ -37,6 +37,8 @@
 //                  mean and the Linear.
 #include "common.h"
 
+#include <cstring>
+
 namespace honk {
 namespace res {
 constexpr int MW = 4;  // waves along M per workgroup
@@ -355,10 +357,12 @@ __device__ __forceinline__ void store4(_Float16* o, f32x4 v) {
 // accesses by the pixel pitch).  The packed weights are zero for channels >= C.
 // ONES: channel C (< CP) holds 1.0 -- the bias channel of the weight-stationary
 // bf16 kernels (pack_block16_kernel)
+// cscale (may be null): the clips' power-of-two scales of the f16x2 path, as conv0m_kernel
 template <int PH, int PW, typename OT, bool SPLIT, bool ONES, int CPM = 48>
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, OT* __restrict__ out,
                                                     const float* __restrict__ w0, int n, int Hin,
-                                                    int Win, int H, int W, int C, int CP) {
+                                                    int Win, int H, int W, int C, int CP,
+                                                    const float* __restrict__ cscale) {
   // SPLIT (bf16x3 activations): per pixel [hi CP][lo CP] bf16, lo = bf16(v - hi)
   constexpr int PPX = SPLIT ? 2 : 1;
   __shared__ __attribute__((aligned(16))) OT stage[256 * CPM * PPX];  // CPM >= CP
@@ -384,6 +388,7 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
     }
     OT* o = stage + threadIdx.x * CP * PPX;
     const float inv = 1.0f / (float)(PH * PW);
+    const float cs = cscale ? cscale[b] : 1.f;
     for (int c4 = 0; c4 < CP; c4 += 4) {
       float v[4];
 #pragma unroll
@@ -404,8 +409,8 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
               for (int kx = 0; kx < 3; ++kx) acc = fmaf(win[a + ky][bb + kx], wr[ky * 3 + kx], acc);
             s += relu_keepnan(acc);
           }
-        v[u] = (PH * PW > 1) ? s * inv : s;
-        if (ONES && c4 + u == C) v[u] = 1.f;
+        v[u] = ((PH * PW > 1) ? s * inv : s) * cs;
+        if (ONES && c4 + u == C) v[u] = cs;
       }
       const f32x4 vv = {v[0], v[1], v[2], v[3]};
       store4(o + c4, vv);
@@ -503,7 +508,9 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
                                                       const float* __restrict__ bout, float* __restrict__ logits,
                                                       int nparts, int HW, int C, int CP, int NL,
                                                       const float* __restrict__ bn_scale,
-                                                      const float* __restrict__ bn_shift) {
+                                                      const float* __restrict__ bn_shift,
+                                                      const float* __restrict__ cscale,
+                                                      const float* __restrict__ oscale) {
   __shared__ float mean[64];
   const int b = blockIdx.x;
   const int c = threadIdx.x;
@@ -511,6 +518,8 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
     const float* p = chsum + (size_t)b * nparts * CP + c;
     float s = 0.f;
     for (int i = 0; i < nparts; ++i) s += p[(size_t)i * CP];
+    // the f16x2 clip scale times the last layer's output exponent (powers of two: exact)
+    if (cscale) s /= cscale[b] * *oscale;
     mean[c] = bn_scale ? fmaf(s / (float)HW, bn_scale[c], bn_shift[c]) : s / (float)HW;
   }
   __syncthreads();
@@ -550,10 +559,12 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 // --------------------------------------------------------------------------- //
 // FWB > 0: the bordered plane width Win + 2 at compile time (40-wide inputs: 42), so a
 // pool member's tap reads take their offset as an immediate
+// cscale (FM 2 only, else null): the clips' power-of-two scales (clip_scale_kernel): the
+// output is s * relu(conv0(x)) (pooled) and channel C holds s instead of 1.0.
 template <int NT, int PH, int PW, int FM, bool ONES, int FWB = 0>
 __global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
                                                      const float* __restrict__ w0, int Hin, int Win, int H, int W,
-                                                     int C) {
+                                                     int C, const float* __restrict__ cscale) {
   constexpr int CP = 16 * NT, P = PH * PW, SP = FM == 1 ? 2 : 1, CB = CP * 2 * SP;
   extern __shared__ __attribute__((aligned(16))) unsigned short c0lds[];  // hi plane, lo plane
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -629,6 +640,8 @@ __global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x
   const int npo = H * W;                 // pooled outputs
   const int ngroups = (npo + 15) >> 4;
   char* oc = (char*)out + (size_t)clip * npo * CB;
+  float cs = 1.f;
+  if constexpr (FM == 2) cs = cscale[clip];
   for (int gi = wave; gi < ngroups; gi += 4) {
     const int q0 = 16 * gi + i16;
     const int q = q0 < npo ? q0 : npo - 1;
@@ -686,7 +699,8 @@ __global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x
           const float q = v * rp;
           v = fmaf(fmaf(-q, (float)P, v), rp, q);
         }
-        if (ONES && co16(NT, n, 4 * g + r) == C) v = 1.f;
+        if constexpr (FM == 2) v *= cs;  // exact: a power of two
+        if (ONES && co16(NT, n, 4 * g + r) == C) v = cs;
         hv[n][r] = (AT)v;
         if constexpr (SP == 2) lv[n][r] = (AT)(v - (float)hv[n][r]);
       }
@@ -751,13 +765,199 @@ __global__ void copy_kernel(const float* __restrict__ src, float* __restrict__ d
 }
 
 // --------------------------------------------------------------------------- //
+// f16x2 range and fitness (the numerics record, HONK_NUM_* in include/honk_hip.h)
+//
+// The f16x2 path stores every pre-BN tensor as ONE fp16: 11 significant bits and a
+// range of 2^-14 .. 65504.  Range: every stored tensor of a clip carries one
+// power-of-two scale s (the clip's scale, clip_scale_kernel): conv0 writes
+// s * relu(conv0(x)) and s itself into the folded-bias channel C, and from there on
+// the scale rides along exactly -- the bias weights multiply channel C (= s), the
+// odd layers' passthrough keeps it, ReLU is positively homogeneous, the residual
+// adds two tensors of the same scale -- so every layer computes s * (its output), a
+// power-of-two multiple of the unscaled arithmetic (bit for bit while the values stay
+// normal), and tail_sum_kernel divides the channel sums by s.
+// s = s_model * 2^-e(clip):
+//  * s_model (pack time) puts M = max over the BatchNorm'd tensors and channels of
+//    |running_mean| + 8 sqrt(running_var) -- the calibrated size of the stored values
+//    (bn2 also bounds conv0's output: relu(conv2) + x0 >= x0) -- just below 2^4, which
+//    leaves 2^12 of headroom to fp16's maximum and 2^18 down to its smallest normal;
+//  * e(clip) (per clip, from its input) = the binades by which the clip's bound
+//    max|x| * max_c sum_t |w0[c][t]| on conv0's output exceeds M: an out-of-range clip
+//    (MFCCs of another scale, c0 in the -1e3..-1e4 range) is scaled down before it is
+//    stored, not clipped to Inf.
+// Fitness (the host policy, honk_res_select_precision): the fp16 rounding of a
+// stored value costs 2^-12 |x|, i.e. 2^-12 |x| / std in the next layer's BatchNorm
+// units, so the error grows with rho = sqrt(mean_c (mean_c^2 + var_c) / var_c); and
+// a folded weight part beyond fp16's range cannot be stored at all (flag).
+// --------------------------------------------------------------------------- //
+#define HONK_NUM_TARGET_EXP 4  // M * s_model < 2^4
+// Weight exponents (f16x2): the folded weights W * invstd of a layer whose input has a
+// large spread (e.g. the residual stream of a model fed MFCCs at 1e3..1e4 scale:
+// std 1e4 -> invstd 1e-4) fall below fp16's smallest normal (6.1e-5), where the
+// (hi, lo) split keeps only ~2^-25 absolute -- a percent of the weight.  So layer i's
+// fragments are packed as W * invstd * 2^kw[i]: an odd layer i and the even layer
+// i + 1 after it take +k / -k (the odd layer's output X_i is stored at 2^k times the
+// residual stream's scale -- its channel-C passthrough and border-bias weights carry
+// the same 2^k, so the scale rides along as the clip scale does -- and the even layer
+// maps it back onto the residual stream), k balancing the two layers' rms weights
+// around their geometric mean, bounded so that X_i keeps the residual stream's fp16
+// headroom (|mean| + 8 std of bn_i times s_model times 2^k < 2^5).  A last odd layer
+// (its output is only summed, in fp32) aims its rms weight at 2^-4.  Models at unit
+// scale get kw = 0 or +-1 (their weights are already O(0.05)).
+// One workgroup: per-layer sums of squares over the fp32 fragments (pack_block_kernel
+// layout), then thread 0.
+__global__ __launch_bounds__(256) void pack_range_kernel(float* __restrict__ rec, const float* __restrict__ bn,
+                                                         const float* __restrict__ w0,
+                                                         const float* __restrict__ frag32, size_t layer_floats,
+                                                         int C, int CP, int NT, int L) {
+  __shared__ double red[256];
+  float* erms = rec + HONK_NUM_KW + L - 1;  // scratch after kw[]: erms[i], i = 1..L
+  const int Q = CP / 16;
+  for (int i = 0; i < L; ++i) {
+    // rms of the folded weights W[co][ci][t] * invstd_{i-1}[ci] (layer 1: no input BN)
+    const float* fr = frag32 + (size_t)i * layer_floats;
+    const float* inv = i > 0 ? bn + (size_t)2 * CP * (i - 1) : nullptr;
+    double q = 0.0;
+    for (size_t e = threadIdx.x; e < layer_floats; e += blockDim.x) {
+      const int j = (int)(e & 3), lane = (int)((e >> 2) & 63);
+      const int qq = (int)((e >> 8) % Q);
+      const int ci = 16 * qq + 4 * (lane >> 4) + j;
+      const double v = (double)fr[e] * (inv && ci < C ? (double)inv[ci] : 1.0);
+      q += v * v;
+    }
+    red[threadIdx.x] = q;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      const double ms = red[0] / ((double)C * C * 9);
+      erms[i + 1] = ms > 0 ? (float)(0.5 * log2(ms)) : 0.f;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  float w0s = 0.f;
+  for (int c = 0; c < C; ++c) {
+    float s = 0.f;
+    for (int t = 0; t < 9; ++t) s += fabsf(w0[c * 9 + t]);
+    w0s = fmaxf(w0s, s);
+  }
+  float M = 0.f, rho = 0.f;
+  int rho_layer = 0;
+  bool bad = !(w0s <= 3.0e38f);
+  for (int i = 0; i < L; ++i) {
+    const float* sc = bn + (size_t)2 * CP * i;  // [scale = invstd][shift = -mean * invstd]
+    double q = 0.0;
+    for (int c = 0; c < C; ++c) {
+      const float inv = sc[c], sh = sc[CP + c];
+      const float m = (fabsf(sh) + 8.f) / inv;  // |mean| + 8 std
+      if (!(m <= 3.0e38f) || !(inv > 0.f)) bad = true;
+      else M = fmaxf(M, m);
+      q += (double)sh * (double)sh;
+    }
+    const float r = (float)sqrt(1.0 + q / (C > 0 ? C : 1));
+    if (!(r <= 3.0e38f)) bad = true;
+    else if (r > rho) {
+      rho = r;
+      rho_layer = i + 1;
+    }
+  }
+  float s = 1.f;
+  if (M > 0.f) {
+    int ex;
+    (void)frexpf(M, &ex);  // M < 2^ex
+    int e = HONK_NUM_TARGET_EXP - ex;
+    if (e > 14) e = 14;
+    if (e < -24) e = -24;
+    s = ldexpf(1.f, e);
+  }
+  // the per-layer weight exponents (layers 1..L, 1-based)
+  float* kw = rec + HONK_NUM_KW;
+  int kout = 0;  // exponent of the last layer's output relative to the residual stream
+  for (int i = 1; i <= L; ++i) kw[i - 1] = 0.f;
+  for (int i = 1; i <= L && !bad; i += 2) {
+    if (i + 1 <= L) {
+      int k = (int)rintf(0.5f * (erms[i + 1] - erms[i]));
+      // X_i's headroom: (|mean| + 8 std of bn_i) * s_model * 2^k < 2^5
+      const float* sc = bn + (size_t)2 * CP * (i - 1);
+      float mx = 0.f;
+      for (int c = 0; c < C; ++c) mx = fmaxf(mx, (fabsf(sc[CP + c]) + 8.f) / sc[c]);
+      int ex = -126;
+      if (mx * s > 0.f) (void)frexpf(mx * s, &ex);
+      if (k > 5 - ex) k = 5 - ex;
+      k = k > 20 ? 20 : k < -20 ? -20 : k;
+      kw[i - 1] = (float)k;
+      kw[i] = (float)-k;
+    } else {
+      int k = (int)rintf(-4.f - erms[i]);
+      k = k > 20 ? 20 : k < -20 ? -20 : k;
+      kw[i - 1] = (float)k;
+      kout = k;
+    }
+  }
+  rec[HONK_NUM_SCALE] = s;
+  rec[HONK_NUM_RANGE] = M;
+  rec[HONK_NUM_W0SUM] = w0s;
+  rec[HONK_NUM_RHO] = bad ? __builtin_nanf("") : rho;
+  // rec[HONK_NUM_F16_OVERFLOW] is set by pack_block16_kernel (which runs after this kernel)
+  rec[HONK_NUM_RHO_LAYER] = (float)rho_layer;
+  rec[HONK_NUM_OUT_SCALE] = ldexpf(1.f, kout);
+  rec[HONK_NUM_VALID] = 1.f;
+}
+
+// The clip's power-of-two scale (see above): one wave per clip; a clip with a
+// non-finite input keeps s_model (its NaN / Inf propagates as in the reference).
+__global__ __launch_bounds__(256) void clip_scale_kernel(const float* __restrict__ x, const float* __restrict__ rec,
+                                                         float* __restrict__ cscale, int n, int hw) {
+  const int lane = threadIdx.x & 63;
+  const int clip = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (clip >= n) return;
+  const float* xc = x + (size_t)clip * hw;
+  float mx = 0.f;
+  bool bad = false;
+  if ((hw & 3) == 0) {
+    const f32x4* x4 = (const f32x4*)xc;
+    for (int i = lane; i < (hw >> 2); i += 64) {
+      const f32x4 v = x4[i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float a = fabsf(v[u]);
+        bad |= !(a <= 3.4e38f);
+        mx = fmaxf(mx, a);
+      }
+    }
+  } else {
+    for (int i = lane; i < hw; i += 64) {
+      const float a = fabsf(xc[i]);
+      bad |= !(a <= 3.4e38f);
+      mx = fmaxf(mx, a);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  bad = __any(bad);
+  float s = rec[HONK_NUM_SCALE];
+  const float M = rec[HONK_NUM_RANGE], bound = mx * rec[HONK_NUM_W0SUM];
+  if (!bad && M > 0.f && bound > M) {
+    const float r = bound / M;
+    int ex = 126;
+    if (r <= 1e37f) (void)frexpf(r, &ex);  // r < 2^ex
+    s = ldexpf(s, -ex);
+  }
+  s = fminf(fmaxf(s, 0x1p-24f), 0x1p14f);  // channel C holds s: an exact fp16 value
+  if (lane == 0) cscale[clip] = s;
+}
+
+// --------------------------------------------------------------------------- //
 // host side
 // --------------------------------------------------------------------------- //
 struct Layout {
   int C, CP, NT, L, NL, prec;
   int Hin, Win, H, W, ph, pw;
   size_t off_conv0, off_layers, layer_floats, off_bn, off_wout, off_bout, off_zeros, off_frag16, frag16_floats,
-      off_fragx3, fragx3_floats, off_fragh, off_bias16, total;
+      off_fragx3, fragx3_floats, off_fragh, off_bias16, off_range, total;
 };
 
 // operand format of the bf16-pipe kernels (res_bf16w.inc): 0 bf16, 1 bf16x3, 2 f16x2;
@@ -807,7 +1007,9 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
   L->off_fragh = L->off_fragx3 + L->fragx3_floats * L->L;
   // folded input-BN bias [L][16 classes][CP] for the bf16 kernel
   L->off_bias16 = L->off_fragh + L->fragx3_floats * L->L;
-  L->total = L->off_bias16 + (size_t)16 * L->CP * L->L;
+  // the numerics record (pack_range_kernel, HONK_NUM_*: 64 header floats, kw[L], scratch[L])
+  L->off_range = L->off_bias16 + round64((size_t)16 * L->CP * L->L);
+  L->total = L->off_range + HONK_NUM_KW + round64((size_t)2 * L->L);
   L->prec = d->precision;
   if (L->prec != HONK_PREC_F32 && L->prec != HONK_PREC_BF16 && L->prec != HONK_PREC_BF16X3 &&
       L->prec != HONK_PREC_F16X2)
@@ -1164,17 +1366,17 @@ static int dispatch_block(const Plan& p, const BlockArgs& a, hipStream_t st) {
 
 template <typename OT, bool SPLIT = false, bool ONES = false>
 static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w0, int64_t n,
-                        hipStream_t st) {
+                        hipStream_t st, const float* cscale = nullptr) {
   const int64_t total = n * L.H * L.W;
   const int blocks = (int)cdiv(total, 256);
 #define HONK_C0(PH, PW)                                                                               \
   if (L.ph == PH && L.pw == PW) {                                                                     \
     if (L.CP <= 48)                                                                                   \
       hipLaunchKernelGGL((conv0_kernel<PH, PW, OT, SPLIT, ONES>), dim3(blocks), dim3(256), 0, st, x, out, w0, \
-                         (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                                  \
+                         (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP, cscale);                          \
     else                                                                                              \
       hipLaunchKernelGGL((conv0_kernel<PH, PW, OT, SPLIT, ONES, 64>), dim3(blocks), dim3(256), 0, st, x, out, \
-                         w0, (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP);                              \
+                         w0, (int)n, L.Hin, L.Win, L.H, L.W, L.C, L.CP, cscale);                      \
     HONK_LAUNCH_CHECK("res conv0_kernel");                                                            \
     return HONK_OK;                                                                                   \
   }
@@ -1192,7 +1394,7 @@ static int launch_conv0(const Layout& L, const float* x, OT* out, const float* w
 // else the VALU kernel.  HONK_CONV0=v forces the VALU kernel (A/B experiments).
 template <int NT, int FM, bool ONES>
 static int launch_conv0m_nt(const Layout& L, const float* x, void* out, const float* w0, int64_t n,
-                            hipStream_t st) {
+                            hipStream_t st, const float* cscale) {
   const unsigned lds = 2u * (unsigned)((L.Hin + 2) * (L.Win + 2)) * 2u;
 #define HONK_C0M(ph_, pw_)                                                                              \
   if (L.ph == ph_ && L.pw == pw_) {                                                                     \
@@ -1201,10 +1403,10 @@ static int launch_conv0m_nt(const Layout& L, const float* x, void* out, const fl
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
     if (L.Win == 40)                                                                                    \
       hipLaunchKernelGGL((conv0m_kernel<NT, ph_, pw_, FM, ONES, 42>), dim3((unsigned)n), dim3(256), lds, st, x, \
-                         (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C);                                \
+                         (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C, cscale);                        \
     else                                                                                                \
       hipLaunchKernelGGL((conv0m_kernel<NT, ph_, pw_, FM, ONES>), dim3((unsigned)n), dim3(256), lds, st, x, \
-                         (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C);                                \
+                         (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C, cscale);                        \
     HONK_LAUNCH_CHECK("res conv0m_kernel");                                                             \
     return HONK_OK;                                                                                     \
   }
@@ -1213,18 +1415,19 @@ static int launch_conv0m_nt(const Layout& L, const float* x, void* out, const fl
   return 1;  // no instance
 }
 template <int FM, bool ONES>
-static int launch_conv0_16(const Layout& L, const float* x, void* out, const float* w0, int64_t n, hipStream_t st) {
+static int launch_conv0_16(const Layout& L, const float* x, void* out, const float* w0, int64_t n, hipStream_t st,
+                           const float* cscale = nullptr) {
   const char* e = getenv("HONK_CONV0");
   const bool valu = e && e[0] == 'v';
   const bool fits = 2L * (L.Hin + 2) * (L.Win + 2) * 2 <= 160 * 1024 && n <= 0x7fffffff;
   if (!valu && fits) {
     int rc = 1;
-    if (L.NT == 1) rc = launch_conv0m_nt<1, FM, ONES>(L, x, out, w0, n, st);
-    else if (L.NT == 2) rc = launch_conv0m_nt<2, FM, ONES>(L, x, out, w0, n, st);
-    else if (L.NT == 3) rc = launch_conv0m_nt<3, FM, ONES>(L, x, out, w0, n, st);
+    if (L.NT == 1) rc = launch_conv0m_nt<1, FM, ONES>(L, x, out, w0, n, st, cscale);
+    else if (L.NT == 2) rc = launch_conv0m_nt<2, FM, ONES>(L, x, out, w0, n, st, cscale);
+    else if (L.NT == 3) rc = launch_conv0m_nt<3, FM, ONES>(L, x, out, w0, n, st, cscale);
     if (rc <= 0) return rc;
   }
-  if constexpr (FM == 2) return launch_conv0<_Float16, false, ONES>(L, x, (_Float16*)out, w0, n, st);
+  if constexpr (FM == 2) return launch_conv0<_Float16, false, ONES>(L, x, (_Float16*)out, w0, n, st, cscale);
   else return launch_conv0<__bf16, FM == 1, ONES>(L, x, (__bf16*)out, w0, n, st);
 }
 
@@ -1278,7 +1481,9 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
   const size_t frl = FM == 0 ? L.frag16_floats : L.fragx3_floats;
   __bf16* R = (__bf16*)workspace;
   __bf16* X = R + act;
-  float* chsum = (float*)(R + 2 * act);
+  float* cscale = (float*)(R + 2 * act);  // [chunk] the f16x2 clip scales (clip_scale_kernel)
+  float* chsum = cscale + round64((size_t)chunk);
+  const float* tail_cs = FM == 2 ? cscale : nullptr;
   const PlanR pr = plan_block16r(L, SP);
   const double layer_flop_per_clip = 2.0 * L.H * L.W * L.C * L.C * 9;
   if (L.L == 0) return fail(HONK_ERR_UNSUPPORTED, "bf16 path needs n_layers >= 1");
@@ -1297,7 +1502,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, 4, L.H * L.W, L.C, L.CP, L.NL, bn_last,
-                         bn_last + L.CP);
+                         bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (whole stack)");
     }
     return HONK_OK;
@@ -1312,8 +1517,13 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
     int parts_last = 0;  // channel-sum partials per clip of the last layer
     for (int64_t c0 = 0; c0 < batch; c0 += chunk) {
       const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
+      if (FM == 2) {
+        hipLaunchKernelGGL(clip_scale_kernel, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, st, x + c0 * L.Hin * L.Win,
+                           packed + L.off_range, cscale, (int)n, L.Hin * L.Win);
+        HONK_LAUNCH_CHECK("res clip_scale_kernel");
+      }
       rc = (FM == 1) ? launch_conv0_16<1, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
-           : (FM == 2) ? launch_conv0_16<2, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+           : (FM == 2) ? launch_conv0_16<2, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st, cscale)
                        : launch_conv0_16<0, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);
       if (rc) return rc;
       int grid = cu_count();
@@ -1416,7 +1626,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, parts_last, L.H * L.W, L.C, L.CP, L.NL,
-                         bn_last, bn_last + L.CP);
+                         bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (weight-stationary)");
     }
     return HONK_OK;
@@ -1459,7 +1669,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, nbc_last * 8, L.H * L.W, L.C, L.CP, L.NL,
-                         bn_last, bn_last + L.CP);
+                         bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16 row-band)");
     }
     return HONK_OK;
@@ -1527,6 +1737,15 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   const int64_t ch = chunk_clips(L, batch);
   if (L.prec != HONK_PREC_F32) {
     const int FM = fmt_of(L.prec), SP = sp_of(FM);
+    if (L.L < 1) {
+      fail(HONK_ERR_UNSUPPORTED, "bf16 / bf16x3 / f16x2 need n_layers >= 1 (use precision f32)");
+      return 0;
+    }
+    if (L.ph * L.pw > 1 && !((L.ph == 2 && L.pw == 2) || (L.ph == 4 && L.pw == 3))) {
+      fail(HONK_ERR_UNSUPPORTED, "bf16 / bf16x3 / f16x2: avg-pool %dx%d has no conv0 kernel (1x1, 2x2, 4x3; "
+           "use precision f32)", L.ph, L.pw);
+      return 0;
+    }
     const PlanR pr = plan_block16r(L, SP);
     if (pr.TH == 0) {
       fail(HONK_ERR_UNSUPPORTED, "bf16/bf16x3: feature-map width %d exceeds the row-band staging plan "
@@ -1545,7 +1764,9 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
       const size_t pw = (size_t)bands_w(L, d, FM, L.L) * 4;  // weight-stationary: [tile][wave]
       if (pw > parts) parts = pw;
     }
-    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + (size_t)ch * parts * L.CP * sizeof(float);
+    // R, X, the clip scales, the channel-sum partials (forward_bf16)
+    return (size_t)2 * ch * L.H * L.W * L.CP * 2 * SP + round64((size_t)ch) * sizeof(float) +
+           (size_t)ch * parts * L.CP * sizeof(float);
   }
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
@@ -1562,34 +1783,47 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
   for (int i = 0; i < n_tensors; ++i)
     if (!t[i]) return fail(HONK_ERR_ARG, "tensor %d is null", i);
   hipStream_t st = (hipStream_t)stream;
+  float* rec = packed + L.off_range;
+  hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(64), 0, st, (const float*)nullptr, rec, 64);
   hipLaunchKernelGGL(pack_conv0_kernel, dim3(cdiv(L.CP * 9, 256)), dim3(256), 0, st, t[0],
                      packed + L.off_conv0, L.C, L.CP);
   HONK_LAUNCH_CHECK("pack_conv0");
   const int nfrag = (int)L.layer_floats;
+  // pass 1: the fp32 fragments and every layer's BatchNorm (scale, shift)
   for (int i = 0; i < L.L; ++i) {
     hipLaunchKernelGGL(pack_block_kernel, dim3(cdiv(nfrag, 256)), dim3(256), 0, st, t[1 + i],
                        packed + L.off_layers + (size_t)i * L.layer_floats, L.C, L.NT);
     HONK_LAUNCH_CHECK("pack_block");
     float* sc = packed + L.off_bn + (size_t)2 * L.CP * i;
-    // bf16: the input BatchNorm (layer i-1's; none for layer 1) folded into
-    // the weights and the border-class bias; layer i-1's BN was packed above
+    hipLaunchKernelGGL(pack_bn_kernel, dim3(1), dim3(64), 0, st, t[1 + L.L + 2 * i],
+                       t[1 + L.L + 2 * i + 1], sc, sc + L.CP, L.C, L.CP);
+    HONK_LAUNCH_CHECK("pack_bn");
+  }
+  // the numerics record: f16x2 scales, fitness, the per-layer weight exponents
+  hipLaunchKernelGGL(pack_range_kernel, dim3(1), dim3(256), 0, st, rec, packed + L.off_bn, packed + L.off_conv0,
+                     packed + L.off_layers, L.layer_floats, L.C, L.CP, L.NT, L.L);
+  HONK_LAUNCH_CHECK("pack_range");
+  // pass 2: the bf16-pipe fragments with the input BatchNorm folded in
+  for (int i = 0; i < L.L; ++i) {
+    // the input BatchNorm (layer i-1's; none for layer 1) folded into the weights and
+    // the border-class bias
     const float* in_bn = (i > 0) ? packed + L.off_bn + (size_t)2 * L.CP * (i - 1) : nullptr;
     const int n16 = ((18 * L.NT + 3) / 4) * L.NT * 64 * 8;
     const float* in_shift = in_bn ? in_bn + L.CP : nullptr;
     const int odd = ((i + 1) & 1);  // layer i + 1 (1-based) is odd
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn, in_shift, odd,
-                       (unsigned short*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, 1, 0);
+                       (unsigned short*)(packed + L.off_frag16 + (size_t)i * L.frag16_floats), L.C, L.NT, 1, 0,
+                       (float*)nullptr, (const float*)nullptr);
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn, in_shift, odd,
-                       (unsigned short*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, 2, 0);
+                       (unsigned short*)(packed + L.off_fragx3 + (size_t)i * L.fragx3_floats), L.C, L.NT, 2, 0,
+                       (float*)nullptr, (const float*)nullptr);
     hipLaunchKernelGGL(pack_block16_kernel, dim3(cdiv(n16, 256)), dim3(256), 0, st, t[1 + i], in_bn, in_shift, odd,
-                       (unsigned short*)(packed + L.off_fragh + (size_t)i * L.fragx3_floats), L.C, L.NT, 2, 1);
+                       (unsigned short*)(packed + L.off_fragh + (size_t)i * L.fragx3_floats), L.C, L.NT, 2, 1,
+                       rec + HONK_NUM_F16_OVERFLOW, (const float*)(rec + HONK_NUM_KW + i));
     HONK_LAUNCH_CHECK("pack_block16");
     hipLaunchKernelGGL(pack_bias16_kernel, dim3(cdiv(16 * L.CP, 256)), dim3(256), 0, st, t[1 + i],
-                       in_bn ? in_bn + L.CP : nullptr, packed + L.off_bias16 + (size_t)16 * L.CP * i, L.C, L.CP);
+                       in_shift, packed + L.off_bias16 + (size_t)16 * L.CP * i, L.C, L.CP);
     HONK_LAUNCH_CHECK("pack_bias16");
-    hipLaunchKernelGGL(pack_bn_kernel, dim3(1), dim3(64), 0, st, t[1 + L.L + 2 * i],
-                       t[1 + L.L + 2 * i + 1], sc, sc + L.CP, L.C, L.CP);
-    HONK_LAUNCH_CHECK("pack_bn");
   }
   const int nw = L.NL * L.C;
   hipLaunchKernelGGL(copy_kernel, dim3(cdiv(nw, 256)), dim3(256), 0, st, t[1 + 3 * L.L],
@@ -1600,6 +1834,80 @@ int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tenso
                      packed + L.off_zeros, 64);
   HONK_LAUNCH_CHECK("pack_copy");
   return HONK_OK;
+}
+
+int honk_res_numerics(const honk_res_desc* d, const float* packed, float* rec, int32_t n, void* stream) {
+  Layout L;
+  int rc = make_layout(d, &L);
+  if (rc) return rc;
+  if (!packed || !rec || n < 1) return fail(HONK_ERR_ARG, "null packed / rec or n < 1");
+  if (n > HONK_NUM_KW + L.L) n = HONK_NUM_KW + L.L;
+  hipStream_t st = (hipStream_t)stream;
+  HONK_HIP_CHECK(hipMemcpyAsync(rec, packed + L.off_range, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));
+  HONK_HIP_CHECK(hipStreamSynchronize(st));
+  return HONK_OK;
+}
+
+// The precision policy (host-only).  "Supported" = the packed forward takes the
+// descriptor in that precision (honk_res_workspace_bytes != 0).
+//  * F32 -> F32.  BF16 (top-1 parity, an explicit choice) -> BF16 where supported.
+//  * F16X2 / AUTO -> F16X2 where its 1e-4 contract holds: the res15 map class (an
+//    unpooled map of >= 4040 pixels -- the spatial mean averages the fp16 rounding --
+//    and >= 32 maps), no folded weight beyond fp16's range, rho <= HONK_F16X2_RHO_MAX;
+//    otherwise the BF16X3 rule.
+//  * BF16X3 -> BF16X3 where supported and rho <= HONK_BF16X3_RHO_MAX, else F32.
+// The rho bounds: exp/f16_range_sim.py (float64 simulation of the kernels' roundings):
+// f16x2 on res15 stays <= 6.4e-5 up to rho 4.9 and failed the bar only at rho >= 5.1
+// (8.4e-5 .. 1.6e-3); bf16x3 carries ~2^5 more significant bits per activation.
+#define HONK_F16X2_RHO_MAX 3.5f
+#define HONK_BF16X3_RHO_MAX 100.f
+static bool prec_supported(const honk_res_desc* d, int p) {
+  honk_res_desc e = *d;
+  e.precision = p;
+  const std::string keep = get_error();
+  const bool ok = honk_res_workspace_bytes(&e, 1) != 0 && honk_res_packed_floats(&e) != 0;
+  set_error("%s", keep.c_str());
+  return ok;
+}
+int honk_res_select_precision(const honk_res_desc* d, const float* rec, int32_t requested, char* note,
+                              size_t note_len) {
+  Layout L;
+  honk_res_desc e = *d;
+  e.precision = HONK_PREC_F32;
+  int rc = make_layout(&e, &L);
+  if (rc) return rc;
+  char buf[256];
+  buf[0] = 0;
+  auto done = [&](int p) {
+    if (note && note_len) snprintf(note, note_len, "%s", buf);
+    return p;
+  };
+  if (requested == HONK_PREC_F32) return done(HONK_PREC_F32);
+  if (requested == HONK_PREC_BF16) {
+    if (prec_supported(d, HONK_PREC_BF16)) return done(HONK_PREC_BF16);
+    snprintf(buf, sizeof buf, "bf16 does not take this shape (%s)", get_error());
+    return done(HONK_PREC_F32);
+  }
+  if (requested != HONK_PREC_F16X2 && requested != HONK_PREC_BF16X3 && requested != HONK_PREC_AUTO)
+    return fail(HONK_ERR_ARG, "unknown precision %d", requested);
+  if (!rec || rec[HONK_NUM_VALID] != 1.f) return fail(HONK_ERR_ARG, "no numerics record (honk_res_numerics)");
+  const float rho = rec[HONK_NUM_RHO];
+  if (requested != HONK_PREC_BF16X3) {
+    const char* why = nullptr;
+    if (!prec_supported(d, HONK_PREC_F16X2)) why = "outside the f16x2 kernels' envelope";
+    else if (L.ph * L.pw > 1 || L.H * L.W < 4040 || L.C < 32)
+      why = "the 1e-4 contract of f16x2 covers unpooled maps of >= 4040 pixels and >= 32 feature maps (res15)";
+    else if (rec[HONK_NUM_F16_OVERFLOW] != 0.f) why = "a folded weight is beyond fp16's range";
+    else if (!(rho <= HONK_F16X2_RHO_MAX)) why = "the stored tensors' mean-to-spread ratio rho exceeds f16x2's bound";
+    if (!why) return done(HONK_PREC_F16X2);
+    snprintf(buf, sizeof buf, "f16x2 not taken: %s (rho %.3g, bound %.3g)", why, (double)rho,
+             (double)HONK_F16X2_RHO_MAX);
+  }
+  if (prec_supported(d, HONK_PREC_BF16X3) && rho <= HONK_BF16X3_RHO_MAX) return done(HONK_PREC_BF16X3);
+  const size_t k = strlen(buf);
+  snprintf(buf + k, sizeof buf - k, "%sbf16x3 not taken (rho %.3g, bound %.3g, %s)", k ? "; " : "", (double)rho,
+           (double)HONK_BF16X3_RHO_MAX, prec_supported(d, HONK_PREC_BF16X3) ? "supported" : "unsupported shape");
+  return done(HONK_PREC_F32);
 }
 
 int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x, float* logits,
@@ -1659,7 +1967,8 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
     } else {
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, p.nbands * MW, L.H * L.W, L.C, L.CP, L.NL,
-                         (const float*)nullptr, (const float*)nullptr);
+                         (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
+                         (const float*)nullptr);
       HONK_LAUNCH_CHECK("res tail_sum_kernel");
     }
   }

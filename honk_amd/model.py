@@ -27,6 +27,8 @@ Forward dispatch:
 """
 from __future__ import annotations
 
+import os
+import warnings
 from enum import Enum
 
 import torch
@@ -117,6 +119,31 @@ def _native_ready(x, module):
     return x.is_cuda and not module.training
 
 
+def default_precision(config):
+    """The eval-forward precision a module starts with, selectable without touching the
+    reference's callers: ``config.get("honk_precision")`` (an optional key, not part of
+    ``_configs``), else the ``HONK_PRECISION`` environment variable, else ``"auto"`` --
+    the fastest mode that holds the north star's 1e-4 logit bar for the model (res:
+    ``honk_res_select_precision``, f16x2 -> bf16x3 -> f32 on the pack-time numerics
+    record; cnn: bf16x3).  ``module.honk_precision`` may be set afterwards as well."""
+    p = None
+    try:
+        p = config.get("honk_precision")
+    except AttributeError:
+        pass
+    return p or os.environ.get("HONK_PRECISION") or "auto"
+
+
+def _warn_reroute(module, requested, chosen, why):
+    seen = module.__dict__.setdefault("_honk_rerouted", set())
+    key = (requested, chosen, why)
+    if key in seen:
+        return
+    seen.add(key)
+    warnings.warn(f"honk_amd: {type(module).__name__} honk_precision={requested!r} runs as {chosen!r}: {why} "
+                  f"(set honk_reroute = False to force {requested!r})", RuntimeWarning, stacklevel=3)
+
+
 def _state_key(tensors, device):
     return (str(device),) + tuple((t.data_ptr(), t._version) for t in tensors)
 
@@ -152,9 +179,15 @@ class SpeechResModel(SerializableModule):
                                pool_w=int(pool[1]) if pool is not None else 0)
         self._honk_packed = None
         self._honk_key = None
-        # "f32": exact fp32 path (1e-4 logit parity); "bf16": bf16 activations/weights
-        # with fp32 accumulation (configs C3/C4; parity = top-1 agreement)
-        self.honk_precision = "f32"
+        # the eval forward's precision (honk_amd/_native.PRECISIONS or "auto"): "f32" (fp32
+        # MFMA), "bf16x3" / "f16x2" (1e-4 logit parity where the pack-time numerics record
+        # admits them -- honk_res_select_precision -- else rerouted with a warning), "bf16"
+        # (top-1 parity), "auto" (the fastest of f16x2 / bf16x3 / f32 that holds 1e-4);
+        # default: default_precision(config)
+        self.honk_precision = default_precision(config)
+        # False: run honk_precision's kernels even where the policy would reroute them
+        # (kernel tests of the f16x2 path on the pooled maps)
+        self.honk_reroute = True
         # training on ROCm tensors: block convs on the gfx950 kernels (False: MIOpen)
         self.honk_native_train = True
 
@@ -243,11 +276,13 @@ class SpeechResModel(SerializableModule):
         ts += [self.output.weight, self.output.bias]
         return ts
 
-    def _desc(self, height, width):
-        if self.honk_precision not in _native.PRECISIONS:
-            raise ValueError(f"honk_precision must be one of {sorted(_native.PRECISIONS)}")
-        return _native.ResDesc(height=height, width=width, precision=_native.PRECISIONS[self.honk_precision],
-                               **self._honk_desc)
+    def _desc(self, height, width, precision=None):
+        p = precision or self.honk_precision
+        if p == "auto":
+            p = "f32"
+        if p not in _native.PRECISIONS:
+            raise ValueError(f"honk_precision must be 'auto' or one of {sorted(_native.PRECISIONS)}")
+        return _native.ResDesc(height=height, width=width, precision=_native.PRECISIONS[p], **self._honk_desc)
 
     def _packed(self, x):
         lib = _native.load()
@@ -259,7 +294,7 @@ class SpeechResModel(SerializableModule):
             if t.device != x.device or t.dtype != torch.float32:
                 raise RuntimeError(f"honk_amd: parameters must be float32 on {x.device} (got {t.dtype} on {t.device})")
         ts = [t.detach().contiguous() for t in ts]
-        desc = self._desc(x.shape[1], x.shape[2])
+        desc = self._desc(x.shape[1], x.shape[2], "f32")  # one layout for every precision
         n = lib.honk_res_packed_floats(desc)
         if n == 0:
             _native.check(-1, "honk_res_packed_floats")
@@ -269,9 +304,67 @@ class SpeechResModel(SerializableModule):
                       "honk_res_pack")
         self._honk_packed, self._honk_key = packed, key
         self._honk_keep = ts  # keep contiguous copies alive until the pack kernels ran
+        self._honk_select = {}
         return packed
 
-    def _native_forward(self, x):
+    def honk_numerics(self, x):
+        """The pack-time numerics record (HONK_NUM_*: the f16x2 scale, range, rho, ...)
+        of this model for inputs shaped like ``x`` (a ROCm tensor)."""
+        with torch.cuda.device(x.device):
+            packed = self._packed(x)
+            return _native.res_numerics(self._desc(x.shape[1], x.shape[2], "f32"), packed, x.device)[0]
+
+    def _run_precision(self, x):
+        """The precision the eval forward runs: honk_precision, or where that is auto /
+        f16x2 / bf16x3 (and honk_reroute), the library's policy on the numerics record
+        (once per pack; a rerouted explicit request warns once)."""
+        req = self.honk_precision
+        if req != "auto" and req not in _native.PRECISIONS:
+            raise ValueError(f"honk_precision must be 'auto' or one of {sorted(_native.PRECISIONS)}")
+        if req in ("f32", "bf16") or (req != "auto" and not self.honk_reroute) or x.dim() != 3:
+            return "f32" if req == "auto" else req
+        with torch.cuda.device(x.device):
+            packed = self._packed(x)
+            key = (req, x.shape[1], x.shape[2])
+            sel = self._honk_select.get(key)
+            if sel is None:
+                desc = self._desc(x.shape[1], x.shape[2], "f32")
+                _, rec = _native.res_numerics(desc, packed, x.device)
+                prec, note = _native.res_select_precision(desc, rec, req)
+                if prec in ("f16x2", "bf16x3"):
+                    prec, note = self._probe(x, prec, note)
+                sel = self._honk_select[key] = (prec, note)
+        prec, note = sel
+        if req != "auto" and prec != req:
+            _warn_reroute(self, req, prec, note)
+        return prec
+
+    # the measured check behind the policy: the reduced modes' logits on the first batch's
+    # first PROBE_CLIPS clips against the fp32 kernels', within PROBE_TOL of the larger of
+    # 1 and the logits' size (half the 1e-4 bar: the rest of the batch and later batches
+    # may sit a little further out); a mode that misses falls to the next (f16x2 -> bf16x3
+    # -> f32).  Once per pack and input shape; a synchronisation.
+    PROBE_CLIPS = 8
+    PROBE_TOL = 5e-5
+
+    def _probe(self, x, prec, note):
+        xs = x[:self.PROBE_CLIPS]
+        ref = self._native_forward(xs, "f32")
+        scale = max(1.0, float(torch.nan_to_num(ref, nan=0.0, posinf=0.0, neginf=0.0).abs().max()))
+        order = ["f16x2", "bf16x3"] if prec == "f16x2" else ["bf16x3"]
+        for p in order:
+            out = self._native_forward(xs, p)
+            same_nonfinite = torch.isfinite(out) == torch.isfinite(ref)
+            both = torch.isfinite(out) & torch.isfinite(ref)
+            err = float((out - ref).abs()[both].max()) if bool(both.any()) else 0.0
+            if bool(same_nonfinite.all()) and err <= self.PROBE_TOL * scale:
+                return p, note
+            note = (f"{note}; " if note else "") + (f"{p} measured {err:.2e} from the fp32 kernels on this "
+                                                    f"model's first {xs.shape[0]} clips (bound "
+                                                    f"{self.PROBE_TOL * scale:.2e})")
+        return "f32", note
+
+    def _native_forward(self, x, precision=None):
         if x.dim() != 3:
             raise RuntimeError(f"SpeechResModel expects [B, H, W] input, got {tuple(x.shape)}")
         if x.dtype != torch.float32:
@@ -280,7 +373,8 @@ class SpeechResModel(SerializableModule):
         lib = _native.load()
         with torch.cuda.device(x.device):
             packed = self._packed(x)
-            desc = self._desc(x.shape[1], x.shape[2])
+            desc = self._desc(x.shape[1], x.shape[2], precision)
+            self.honk_last_precision = precision or self.honk_precision
             B = x.shape[0]
             out = torch.empty(B, self._honk_desc["n_labels"], dtype=torch.float32, device=x.device)
             if B == 0:
@@ -294,30 +388,31 @@ class SpeechResModel(SerializableModule):
                           "honk_res_forward")
         return out
 
-    def _native_fits(self, x):
+    def _native_fits(self, x, precision):
         """None if the packed forward (honk_res_forward) takes this model and input shape,
         else the library's reason (host-only queries, cached per precision and map size)."""
-        key = (self.honk_precision, x.shape[1], x.shape[2])
+        key = (precision, x.shape[1], x.shape[2])
         fits = self.__dict__.setdefault("_honk_fits", {})
         if key not in fits:
             lib = _native.load()
-            desc = self._desc(x.shape[1], x.shape[2])
+            desc = self._desc(x.shape[1], x.shape[2], precision)
             ok = lib.honk_res_packed_floats(desc) != 0 and lib.honk_res_workspace_bytes(desc, 1) != 0
             fits[key] = None if ok else lib.honk_last_error().decode(errors="replace")
         return fits[key]
 
     def forward(self, x):
         if _native_ready(x, self):
-            why = self._native_fits(x) if x.dim() == 3 else None
+            prec = self._run_precision(x) if x.dim() == 3 else None
+            why = self._native_fits(x, prec) if x.dim() == 3 else None
             if why is not None:
                 # beyond the packed kernels' envelope (more than 64 maps in f32 / 48 in bf16,
                 # maps wider than the bf16 staging plan): the same forward on the layer-level
                 # kernels (native stem, block convs, mean, Linear; eval BatchNorm and the
                 # residual adds as device elementwise ops), in fp32
                 _conv3x3.warn_fallback(self, f"the eval forward of {tuple(x.shape[1:])} inputs in "
-                                             f"{self.honk_precision} ({why}): layer-level fp32 kernels instead")
+                                             f"{prec} ({why}): layer-level fp32 kernels instead")
                 return self._torch_forward(x, native_convs=True)
-            return self._native_forward(x)
+            return self._native_forward(x, prec)
         return self._torch_forward(x, native_convs=x.is_cuda and self.honk_native_train)
 
 
@@ -400,8 +495,10 @@ class SpeechModel(SerializableModule):
         self.dropout = nn.Dropout(dropout_prob)
         self._honk_desc = desc
         # "f32": fp32 MFMA; "bf16x3": operands split into bf16 hi/lo pairs on the
-        # bf16 MFMA pipe (same 1e-4 logit bar; tests/test_gpu_cnn_x3.py)
-        self.honk_precision = "f32"
+        # bf16 MFMA pipe (same 1e-4 logit bar; tests/test_gpu_cnn_x3.py); "auto" =
+        # bf16x3; default: default_precision(config)
+        self.honk_precision = default_precision(config)
+        self.honk_reroute = True
         # training on ROCm tensors: convs + ReLU and max-pools on the gfx950 kernels (False: MIOpen)
         self.honk_native_train = True
 
@@ -472,9 +569,17 @@ class SpeechModel(SerializableModule):
             if t is not None and (t.device != x.device or t.dtype != torch.float32):
                 raise RuntimeError(f"honk_amd: parameters must be float32 on {x.device}")
         ts = [t.detach().contiguous() if t is not None else None for t in ts]
-        if self.honk_precision not in ("f32", "bf16x3"):
-            raise ValueError("SpeechModel.honk_precision must be 'f32' or 'bf16x3'")
-        desc = _native.CnnDesc(**d, precision=_native.PRECISIONS[self.honk_precision])
+        prec = self.honk_precision
+        if prec == "auto":
+            prec = "bf16x3"
+        elif prec == "f16x2" and self.honk_reroute:
+            # the cnn path has no fp16 kernels; bf16x3 holds the same 1e-4 bar
+            _warn_reroute(self, prec, "bf16x3", "SpeechModel has no f16x2 kernels")
+            prec = "bf16x3"
+        if prec not in ("f32", "bf16x3"):
+            raise ValueError("SpeechModel.honk_precision must be 'auto', 'f32' or 'bf16x3'")
+        self.honk_last_precision = prec
+        desc = _native.CnnDesc(**d, precision=_native.PRECISIONS[prec])
         B = x.shape[0]
         with torch.cuda.device(x.device):
             out = torch.empty(B, d["n_labels"], dtype=torch.float32, device=x.device)

@@ -65,12 +65,17 @@ typedef struct honk_res_desc {
 #define HONK_PREC_BF16 1
 #define HONK_PREC_BF16X3 2
 /* fp16 activations (RNE), weights (input BN folded) as fp16 hi + lo, products
-   w_hi*x + w_lo*x on fp16 MFMA, fp32 accumulate: ~11-bit activations.  Runs on the
-   weight-stationary / pair kernels only (n_maps <= 48 with a zero-padding channel,
-   (pooled) width < 64; HONK_ERR_UNSUPPORTED otherwise).  Logit error: within the
-   1e-4 bar on res15 (simulated <= 3.8e-5, measured on the goldens); up to ~2e-4 on
-   the pooled res8 / res26 maps, which average over fewer pixels. */
+   w_hi*x + w_lo*x on fp16 MFMA, fp32 accumulate: ~11-bit activations, each clip's
+   stored tensors scaled by a power of two that keeps them inside fp16's range (see
+   HONK_NUM_SCALE).  Runs on the weight-stationary / pair kernels only (n_maps <= 48
+   with a zero-padding channel, (pooled) width < 64; HONK_ERR_UNSUPPORTED otherwise).
+   Logit error: within the 1e-4 bar on res15 (simulated <= 3.8e-5, measured on the
+   goldens); up to ~2e-4 on the pooled res8 / res26 maps, which average over fewer
+   pixels -- honk_res_select_precision routes those to BF16X3. */
 #define HONK_PREC_F16X2 3
+/* Not a kernel format: honk_res_select_precision's request for "the fastest mode that
+   holds the 1e-4 logit bar for this model" (f16x2 -> bf16x3 -> f32). */
+#define HONK_PREC_AUTO 4
 
 /* number of floats of the packed (kernel-layout) weight buffer */
 size_t honk_res_packed_floats(const honk_res_desc* d);
@@ -98,6 +103,57 @@ int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, i
  */
 int honk_res_pack(const honk_res_desc* d, const float* const* tensors, int32_t n_tensors,
                   float* packed, void* stream);
+/*
+ * The numerics record honk_res_pack writes into `packed` (device; read by the f16x2
+ * forward, and by the host through honk_res_numerics):
+ *   HONK_NUM_SCALE    s_model, the power-of-two activation scale of the f16x2 path:
+ *                     M * s_model < 2^4 (each clip stores s * (its pre-BN tensors) with
+ *                     s = s_model, lowered by the binades its input's conv0 bound
+ *                     max|x| * HONK_NUM_W0SUM exceeds M -- fp16's range follows the clip)
+ *   HONK_NUM_RANGE    M = max over layers / channels of |running_mean| + 8 sqrt(running_var)
+ *   HONK_NUM_W0SUM    max_c sum_t |conv0.weight[c][0][t]|
+ *   HONK_NUM_RHO      max over layers of sqrt(mean_c (mean_c^2 + var_c) / var_c): the RMS
+ *                     size of a stored tensor in its own BatchNorm units (the factor by
+ *                     which the storage rounding grows in the next layer); NaN if a
+ *                     statistic is not finite
+ *   HONK_NUM_F16_OVERFLOW  1 if a folded weight (W * invstd, or a border-bias weight)
+ *                     has no finite fp16 (hi, lo) split
+ *   HONK_NUM_RHO_LAYER the layer (1-based) of HONK_NUM_RHO
+ *   HONK_NUM_VALID    1 once the record is written
+ *   HONK_NUM_OUT_SCALE 2^kw[L] for an odd n_layers (the last layer's output relative to
+ *                     the residual stream's scale), else 1
+ *   [HONK_NUM_KW + i] kw[i+1], the f16x2 weight exponent of conv{i+1}: its folded weights
+ *                     are packed times 2^kw, an odd layer and the even layer after it
+ *                     taking +k / -k (keeps weights of layers fed by a wide-spread tensor
+ *                     out of fp16's subnormal range; 0 / +-1 at unit scale)
+ */
+#define HONK_NUM_SCALE 0
+#define HONK_NUM_RANGE 1
+#define HONK_NUM_W0SUM 2
+#define HONK_NUM_RHO 3
+#define HONK_NUM_F16_OVERFLOW 4
+#define HONK_NUM_RHO_LAYER 5
+#define HONK_NUM_VALID 6
+#define HONK_NUM_OUT_SCALE 7
+#define HONK_NUM_COUNT 8
+#define HONK_NUM_KW 64
+/* Copy the first n (at most HONK_NUM_KW + n_layers) record entries to HOST memory rec[]:
+   enqueues the copy on `stream` and SYNCHRONISES it (once per pack, not on the forward
+   path). */
+int honk_res_numerics(const honk_res_desc* d, const float* packed, float* rec, int32_t n, void* stream);
+/*
+ * Host-only precision policy: the precision honk_res_forward should run for the
+ * `requested` one (HONK_PREC_*, HONK_PREC_AUTO) given the model's record (rec from
+ * honk_res_numerics; may be NULL for F32 / BF16).  F32 -> F32; BF16 (top-1 parity, an
+ * explicit choice) -> BF16 where the kernels take the shape, else F32; F16X2 / AUTO ->
+ * F16X2 where its 1e-4 contract holds (unpooled maps of >= 4040 pixels and >= 32 maps,
+ * no folded weight beyond fp16's range, HONK_NUM_RHO <= 3.5), else as BF16X3; BF16X3
+ * -> BF16X3 where supported and HONK_NUM_RHO <= 100, else F32.  note (may be NULL)
+ * receives why a requested format was not taken ("" when it was).  Returns the
+ * precision (>= 0) or a HONK_ERR_* code.
+ */
+int honk_res_select_precision(const honk_res_desc* d, const float* rec, int32_t requested, char* note,
+                              size_t note_len);
 /* x: [batch, height, width] fp32;  logits: [batch, n_labels] fp32 (eval-mode forward) */
 int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x, float* logits,
                      int64_t batch, void* workspace, size_t workspace_bytes, void* stream);

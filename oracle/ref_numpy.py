@@ -254,6 +254,30 @@ def res_forward(params, cfg, x, acc=np.float64, trace=None):
     return linear(x, params["output.weight"], params["output.bias"])   # :121
 
 
+def res_prebn_max(params, cfg, x):
+    """max |value| over the tensors the packed res kernels store (conv0's output and
+    every layer's pre-BN output, model.py:107-116), float64 -- the range an activation
+    storage format must cover (tests/golden/make_range_golden.py)."""
+    x = np.asarray(x, dtype=np.float64)[:, None]
+    mx, old_x = 0.0, None
+    for i in range(int(cfg["n_layers"]) + 1):
+        if i == 0:
+            y = relu(conv2d(x, params["conv0.weight"], padding=(1, 1)))
+            if "res_pool" in cfg:
+                y = avg_pool2d(y, tuple(cfg["res_pool"]))
+            old_x = x = y
+        else:
+            d = res_dilation(cfg, i)
+            y = relu(conv2d(x, params[f"conv{i}.weight"], padding=(d, d), dilation=(d, d)))
+            x = y + old_x if i % 2 == 0 else y
+            if i % 2 == 0:
+                old_x = x
+        mx = max(mx, float(np.nanmax(np.abs(x))))
+        if i > 0:
+            x = batch_norm_eval(x, params[f"bn{i}.running_mean"], params[f"bn{i}.running_var"])
+    return mx
+
+
 def cnn_forward(params, cfg, x, acc=np.float64):
     """SpeechModel.forward in eval mode (dropout = identity), model.py:186-205."""
     tf = bool(cfg.get("tf_variant"))

@@ -28,6 +28,7 @@ def module(cfg, params, name):
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     m = m.eval().to(DEV)
     m.honk_precision = "bf16x3"
+    m.honk_reroute = False
     return m
 
 

@@ -38,6 +38,7 @@ def module(cfg, params, name, prec="f16x2"):
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     m = m.eval().to(DEV)
     m.honk_precision = prec
+    m.honk_reroute = False   # the f16x2 kernels themselves, pooled maps included (policy: test_gpu_range.py)
     return m
 
 

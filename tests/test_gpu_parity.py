@@ -28,6 +28,7 @@ def _need_gpu():
 def module(cfg, params, name):
     m = hm.find_model(name)(cfg)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    m.honk_precision = "f32"   # this file pins the fp32 kernels; the default ("auto"): test_gpu_range.py
     return m.eval().to(DEV)
 
 
@@ -91,6 +92,7 @@ def test_res_wide_models_run_on_layer_kernels():
         params, x = _res_case(cfg, 3, seed=maps)
         m = module(cfg, params, "res8")
         m.honk_precision = prec
+        m.honk_reroute = False   # the requested kernels' envelope itself (auto / reroute: test_gpu_range.py)
         assert _native.load().honk_res_packed_floats(m._desc(101, 40)) == 0 or \
             _native.load().honk_res_workspace_bytes(m._desc(101, 40), 1) == 0
         import warnings
@@ -258,6 +260,7 @@ def test_res_wide_input_envelope(width, prec, ok):
     params = orc.calibrate_bn(params, cfg, x)
     m = module(cfg, params, "res15")
     m.honk_precision = prec
+    m.honk_reroute = False
     if not ok:
         # the packed forward refuses; the module runs the layer-level fp32 kernels
         assert _native.load().honk_res_workspace_bytes(m._desc(101, width), 1) == 0
