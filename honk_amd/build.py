@@ -24,10 +24,32 @@ def hipcc():
 def needs_build():
     if not os.path.exists(LIB):
         return True
+    tmp = os.path.join(HERE, "_build")
+    for src in SOURCES:  # the device assembly the spill guard reads
+        if src.endswith(".hip") and not os.path.exists(
+                os.path.join(tmp, src.rsplit(".", 1)[0] + "-hip-amdgcn-amd-amdhsa-gfx950.s")):
+            return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
         os.path.join(HERE, "..", "include", "honk_hip.h")]
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+
+
+def check_spills(build_dir):
+    """Fail the build on a SPLIT register spill (a reload that restores part of a tuple an
+    MFMA or other instruction then reads whole: the shape of the LLVM miscompile that gave
+    wrong bf16 logits in round 4) -- tools/check_spills.py over the device assembly."""
+    sys.path.insert(0, os.path.join(HERE, "..", "tools"))
+    try:
+        import check_spills as cs
+    finally:
+        sys.path.pop(0)
+    paths = [os.path.join(build_dir, f) for f in sorted(os.listdir(build_dir))
+             if f.endswith("-hip-amdgcn-amd-amdhsa-gfx950.s")]
+    bad = cs.check_files(paths, verbose=False)
+    if bad:
+        raise RuntimeError("split register spills (tools/check_spills.py):\n" +
+                           "\n".join(f"  {os.path.basename(p)}: {k}: {d}" for p, k, d in bad))
 
 
 def build(force=False, verbose=False):
@@ -36,8 +58,10 @@ def build(force=False, verbose=False):
     objs = []
     tmp = os.path.join(HERE, "_build")
     os.makedirs(tmp, exist_ok=True)
+    # -save-temps=obj keeps each file's device assembly (<src>-hip-amdgcn-amd-amdhsa-gfx950.s in
+    # _build/): the code the objects hold, which the spill guard below reads
     base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-            "-I", os.path.join(HERE, "..", "include")]
+            "-save-temps=obj", "-I", os.path.join(HERE, "..", "include")]
     procs = []
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))] + [
         os.path.join(HERE, "..", "include", "honk_hip.h")]
@@ -45,7 +69,8 @@ def build(force=False, verbose=False):
         obj = os.path.join(tmp, src.rsplit(".", 1)[0] + ".o")
         objs.append(obj)
         # incremental: an object newer than its source and every shared header is kept
-        if not force and os.path.exists(obj) and all(
+        asm = os.path.join(tmp, src.rsplit(".", 1)[0] + "-hip-amdgcn-amd-amdhsa-gfx950.s")
+        if not force and os.path.exists(obj) and (os.path.exists(asm) or not src.endswith(".hip")) and all(
                 os.path.getmtime(obj) > os.path.getmtime(p) for p in [os.path.join(CSRC, src)] + headers):
             continue
         cmd = base + (["-x", "hip"] if src.endswith(".cpp") else []) + ["-c", os.path.join(CSRC, src), "-o", obj]
@@ -58,6 +83,7 @@ def build(force=False, verbose=False):
             raise RuntimeError(f"hipcc failed on {src}:\n{out}")
         if verbose and out.strip():
             print(out)
+    check_spills(tmp)
     link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:

@@ -312,7 +312,9 @@ class _ResTail(torch.autograd.Function):
         h = h.contiguous()
         old = old.contiguous() if old is not None else None
         B, C, H, W = h.shape
-        y = torch.empty_like(h)
+        # fold: no y -- a zero-storage placeholder of its shape (a stray read sees one
+        # element, not a stale full-size buffer, and nothing is allocated for it)
+        y = torch.empty((), dtype=h.dtype, device=h.device).expand(B, C, H, W) if fold else torch.empty_like(h)
         mean = torch.empty(C, dtype=torch.float32, device=h.device)
         invstd = torch.empty_like(mean)
         ptr = (lambda t: t.data_ptr() if t is not None else None)

@@ -194,6 +194,14 @@ class GradAllReduce:
         if self.count == len(self.flat.params):
             self.work = dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM, async_op=True)
 
+    def reset(self):
+        """Start a step: drop any count / collective a previous step left (e.g. one that
+        raised between backward and wait()), so every rank's next all-reduce matches."""
+        if self.work is not None:
+            self.work.wait()
+        self.work = None
+        self.count = 0
+
     def wait(self) -> float:
         if self.world == 1:
             return 1.0

@@ -222,6 +222,10 @@ class SpeechResModel(SerializableModule):
                 box = {}
                 old = old_x if i % 2 == 0 else None
                 h = _conv3x3.conv3x3(x, conv.weight, d, old=old, box_out=box, box_in=box_in)
+                if box_in is not None and "fold" in box_in:
+                    # the tail below folded its BatchNorm for this conv, which did not take it:
+                    # x is a placeholder, so stop rather than compute from it
+                    raise RuntimeError("honk_amd: a folded BatchNorm was not consumed by the next conv")
                 bn = getattr(self, "bn{}".format(i))
                 # the BatchNorm goes into the next block's conv when that conv takes it
                 # (the last block's output feeds the head: materialized)

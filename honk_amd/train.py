@@ -168,10 +168,7 @@ def train(config, datasets=None):
     optimizer = _sgd(flat, config, config["lr"][0])
     schedule_steps = config["schedule"]  # the caller's list, extended in place (utils/train.py:100-101)
     schedule_steps.append(np.inf)
-    sched_idx = 0
     criterion = head_train.CrossEntropyLoss()  # nn.CrossEntropyLoss(); native on ROCm tensors
-    max_acc = 0
-    best_model = None
 
     if world > 1:
         sampler = data.distributed.DistributedSampler(train_set, num_replicas=world, rank=rank, shuffle=True,
@@ -185,13 +182,26 @@ def train(config, datasets=None):
     dev_loader = data.DataLoader(dev_set, batch_size=min(len(dev_set), 16), shuffle=False,
                                  collate_fn=getattr(dev_set, "collate_fn", None))
     test_loader = _whole_set_loader(test_set)
-    step_no = 0
+    try:
+        best_model = _train_epochs(config, model, train_set, dev_set, train_loader, dev_loader, sampler, flat,
+                                   fbuf, reducer, optimizer, schedule_steps, criterion, log)
+    finally:
+        reducer.remove()  # no gradient hooks (and no stray all-reduce) outlive train()
+    if log:
+        evaluate(config, best_model, test_loader)
+
+
+def _train_epochs(config, model, train_set, dev_set, train_loader, dev_loader, sampler, flat, fbuf, reducer,
+                  optimizer, schedule_steps, criterion, log):
+    """utils/train.py:123-162: the epochs of train(); returns the best model on dev."""
+    sched_idx, step_no, max_acc, best_model = 0, 0, 0, None
     for epoch_idx in range(config["n_epochs"]):
         if sampler is not None:
             sampler.set_epoch(epoch_idx)
         for model_in, labels in train_loader:
             model.train()
             optimizer.zero_grad()
+            reducer.reset()
             labels_host = labels
             # a DeviceSpeechDataset batch is clip indices: augmentation + MFCC on the device
             model_in = batch_input(train_set, model_in)
@@ -235,8 +245,7 @@ def train(config, datasets=None):
                     print("saving best model...")
                     model.save(config["output_file"])
                 best_model = copy.deepcopy(model)
-    if log:
-        evaluate(config, best_model, test_loader)
+    return best_model
 
 
 def default_run_config(output_file=None):

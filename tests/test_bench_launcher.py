@@ -138,3 +138,21 @@ def test_spawn_parent_never_initialises_hip(tmp_path):
     p = subprocess.run([sys.executable, "-c", drv, "3"], env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 2, p.stderr
     assert "only 2 visible GPU(s)" in p.stderr
+
+
+def test_modes_summary_keeps_every_number():
+    """The bench line ends with a compact per-mode summary (VERDICT r4 weak #6)."""
+    import bench
+    res = {"dtype": "f16x2", "value": 3.0e5, "roofline": {"frac": 0.45},
+           "bf16x3_mode": {"dtype": "bf16x3", "value": 1.9e5, "roofline": {"frac": 0.44}},
+           "f32_mode": {"dtype": "f32", "value": 5.7e4, "roofline": {"frac": 0.7}},
+           "c2_cnn_trad_pool2": {"f32_mode": {"value": 5.8e5, "dtype": "f32", "roofline": {"frac": 0.71}},
+                                 "bf16x3_mode": {"value": 1.6e6, "dtype": "bf16x3", "roofline": {"frac": 0.4}}},
+           "c3_res8_bf16": {"value": 7e6, "dtype": "bf16", "roofline": {"frac": 0.28}},
+           "c5_res26_narrow_train": {"value": 1.26e5, "dtype": "f32", "roofline": {"frac": 0.38}},
+           "cpu_baseline": {"value": 97.3, "cores": 16}}
+    m = bench.modes_summary(res, "res15")
+    assert m["res15_f16x2 (headline)"] == {"value": 3.0e5, "dtype": "f16x2", "frac": 0.45}
+    assert set(m) == {"res15_f16x2 (headline)", "res15_bf16x3", "res15_f32", "c2_cnn-trad-pool2_f32",
+                      "c2_cnn-trad-pool2_bf16x3", "c3_res8_bf16", "c5_res26_narrow_train", "cpu_baseline"}
+    assert bench._plan_str(["block16p_kernel"] * 6 + ["block16l_kernel"]) == "block16p_kernel x6 + block16l_kernel x1"

@@ -205,3 +205,45 @@ def test_flat_buffers_rehome_keeps_state_dict():
     m.train()(torch.randn(3, 101, 40))
     assert not torch.equal(before, fb.data)
     assert m.bn1.running_mean.data_ptr() == fb.data.data_ptr()
+
+
+def _remove_worker(rank, world, port, out):
+    """GradAllReduce.remove(): no hook outlives the training loop; reset():
+    a step that raised between backward and wait() leaves no stale count or collective."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+    orig = dist.all_reduce
+
+    def wrap(*a, **k):
+        calls.append("all_reduce")
+        return orig(*a, **k)
+    dist.all_reduce = wrap
+    m = _model(seed=0)
+    flat = FlatParams(m)
+    red = hd.GradAllReduce(flat)
+    x, y = _batch(8)
+    m.train()
+    torch.nn.functional.cross_entropy(m(x), y).backward()   # a step that "raised" before wait()
+    n_raised = len(calls)
+    red.reset()
+    flat.zero_grad()
+    torch.nn.functional.cross_entropy(m(x), y).backward()
+    red.wait()
+    n_step = len(calls)
+    red.remove()
+    flat.zero_grad()
+    torch.nn.functional.cross_entropy(m(x), y).backward()   # after remove(): no collective
+    out[rank] = (n_raised, n_step, len(calls), red.count)
+    dist.all_reduce = orig
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_reset_and_remove():
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_remove_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    for r in (0, 1):
+        assert res[r] == (1, 2, 2, 0), res[r]
