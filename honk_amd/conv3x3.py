@@ -312,14 +312,16 @@ class _ResTail(torch.autograd.Function):
         h = h.contiguous()
         old = old.contiguous() if old is not None else None
         B, C, H, W = h.shape
-        # fold: no y -- a zero-storage placeholder of its shape (a stray read sees one
-        # element, not a stale full-size buffer, and nothing is allocated for it)
-        y = torch.empty((), dtype=h.dtype, device=h.device).expand(B, C, H, W) if fold else torch.empty_like(h)
         mean = torch.empty(C, dtype=torch.float32, device=h.device)
         invstd = torch.empty_like(mean)
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         st = _native.stream_handle(h.device)
         mask = box.pop("mask", None) if box is not None else None
+        # fold (only on the masked path, whose conv epilogue supplied the statistics): no y --
+        # a zero-storage placeholder of its shape (a stray read sees one element, not a stale
+        # full-size buffer, and nothing is allocated); every other path writes a full y
+        fold = bool(fold) and mask is not None
+        y = torch.empty((), dtype=h.dtype, device=h.device).expand(B, C, H, W) if fold else torch.empty_like(h)
         if mask is not None:
             # h holds s = relu(h) [+ old] from the conv's epilogue (and old was read there)
             STATS_USED["fwd"] += 1
