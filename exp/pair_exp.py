@@ -1,0 +1,238 @@
+"""Experiment builds of the f16x2 res15 pair kernel (block16p_kernel<3, 1, 4, 4, 1, 2>).
+
+    python exp/pair_exp.py build VARIANT ...     -> exp/_pair/<variant>/libhonk_hip.so
+    python exp/pair_exp.py time VARIANT ...      (GPU box: rocprofv3 kernel stats per variant)
+
+A variant = patches to a copy of csrc/res_bf16p.inc (and res.hip), compiled with every
+kernel instantiation the f16x2 res15 forward does not launch cut out of the copy's
+res.hip (the "reduce" patches: ~5x faster to compile).  Ablation variants compute WRONG
+results by construction (timing only, never shipped); every memory access stays in
+bounds (skipped work, frozen geometry), so they are as safe to run as the product.
+"""
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "exp", "_pair")
+NEVER = "a.H == 12345"  # runtime-false: the compiler keeps the code shape around it
+
+REDUCE = [
+    ("""  HONK_W(1, 0) HONK_W(2, 0) HONK_W(3, 0)
+  HONK_W(1, 1) HONK_W(2, 1) HONK_W(3, 1)
+  HONK_W(1, 2) HONK_W(2, 2) HONK_W(3, 2)""", "  HONK_W(3, 2)"),
+    ("""  if (SP == 1) {
+    if (p.NT == 1 && p.MT == g16r_mt(1, 1)) return launch_block16r<1, g16r_mt(1, 1), 1>(a, st);
+    if (p.NT == 2 && p.MT == g16r_mt(2, 1)) return launch_block16r<2, g16r_mt(2, 1), 1>(a, st);
+    if (p.NT == 3 && p.MT == g16r_mt(3, 1)) return launch_block16r<3, g16r_mt(3, 1), 1>(a, st);
+  } else {
+    if (p.NT == 1 && p.MT == g16r_mt(1, 2)) return launch_block16r<1, g16r_mt(1, 2), 2>(a, st);
+    if (p.NT == 2 && p.MT == g16r_mt(2, 2)) return launch_block16r<2, g16r_mt(2, 2), 2>(a, st);
+    if (p.NT == 3 && p.MT == g16r_mt(3, 2)) return launch_block16r<3, g16r_mt(3, 2), 2>(a, st);
+  }""", ""),
+    ("""  HONK_CASE(1, 2) HONK_CASE(1, 3) HONK_CASE(1, 4) HONK_CASE(1, 5) HONK_CASE(1, 6)
+  HONK_CASE(2, 2) HONK_CASE(2, 3) HONK_CASE(2, 4) HONK_CASE(2, 5) HONK_CASE(2, 6)
+  HONK_CASE(3, 2) HONK_CASE(3, 3) HONK_CASE(3, 4) HONK_CASE(3, 5)
+  HONK_CASE(4, 2)""", ""),
+    ("""    if (L.NT == 1) rc = launch_conv0m_nt<1, FM, ONES>(L, x, out, w0, n, st, cscale);
+    else if (L.NT == 2) rc = launch_conv0m_nt<2, FM, ONES>(L, x, out, w0, n, st, cscale);
+    else if (L.NT == 3)""", "    if (L.NT == 3)"),
+    ("""  if constexpr (FM == 2) return launch_conv0<_Float16, false, ONES>(L, x, (_Float16*)out, w0, n, st, cscale);
+  else return launch_conv0<__bf16, FM == 1, ONES>(L, x, (__bf16*)out, w0, n, st);""", "  return HONK_ERR_UNSUPPORTED;"),
+    ("      rc = launch_conv0_16<0, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);\n      if (rc) return rc;\n"
+     "      rc = L.NT == 3 ? launch_block16n<3>(L, R, frb, frl, chsum, n, st) : launch_block16n<2>(L, R, frb, frl, chsum, n, st);",
+     "      rc = HONK_ERR_UNSUPPORTED;"),
+    ("""      rc = (FM == 1) ? launch_conv0_16<1, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+           : (FM == 2) ? launch_conv0_16<2, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st, cscale)
+                       : launch_conv0_16<0, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);""",
+     """      rc = launch_conv0_16<2, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st, cscale);"""),
+    ("""            if (FM == 1 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9, 1>), gd, bd, 0, st, pa);
+            else if (FM == 1 && pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10, 1>), gd, bd, 0, st, pa);
+            else if (FM == 1) hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9, 1>), gd, bd, 0, st, pa);
+            else if (FM == 2 && pp.ppr == 4)""", "            if (FM == 2 && pp.ppr == 4)"),
+    ("""            else if (FM == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 1, 2>), gd, bd, 0, st, pa);
+            else if (pp.ppr == 4 && pp.ns == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
+            else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1>), gd, bd, 0, st, pa);
+            else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 1>), gd, bd, 0, st, pa);""", ""),
+    ("""            if (FM == 1) hipLaunchKernelGGL((block16l_kernel<3, 2, 9, 9, 2>), gd, bd, 0, st, pa);
+            else if (FM == 2) hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2, 2>), gd, bd, 0, st, pa);
+            else hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);""",
+     """            if (FM == 2) hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2, 2>), gd, bd, 0, st, pa);"""),
+    ("""      rc = (SP == 2) ? launch_conv0_16<1, false>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
+                     : launch_conv0_16<0, false>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);""",
+     "      rc = HONK_ERR_UNSUPPORTED;"),
+    ("    rc = launch_conv0(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st);", "    rc = HONK_ERR_UNSUPPORTED;"),
+]
+
+# ---- variants: patches to res_bf16p.inc ---------------------------------------------
+EPI = ("        if constexpr ((KE + E < KSA ? KE + E : KSA - 1) == S) epi_step(",
+       f"        if constexpr ((KE + E < KSA ? KE + E : KSA - 1) == S) if ({NEVER}) epi_step(")
+RES = ("      if constexpr (ISB && S == 0) res_loads(rvs[PAR], cur.pix);",
+       f"      if constexpr (ISB && S == 0) if ({NEVER}) res_loads(rvs[PAR], cur.pix);")
+DMA = ("        dma(widx ? roff[rb] : roff[ra],", f"        if ({NEVER}) dma(widx ? roff[rb] : roff[ra],")
+BAR = ("      __builtin_amdgcn_s_barrier();\n      asm volatile(\"\" ::: \"memory\");\n      if constexpr (TBL) {",
+       f"      if ({NEVER}) __builtin_amdgcn_s_barrier();\n      asm volatile(\"\" ::: \"memory\");\n      if constexpr (TBL) {{")
+WALK = ("      if constexpr (S == KW) walk_adv(wk);", f"      if constexpr (S == KW) if ({NEVER}) walk_adv(wk);")
+GEO = ("      if constexpr (S == KG) nxt = geo(wk);", f"      if constexpr (S == KG) if ({NEVER}) nxt = geo(wk);")
+MAXR = ("common.h", "__device__ __forceinline__ float relu_keepnan(float x) { return x <= 0.f ? 0.f : x; }",
+        "__device__ __forceinline__ float relu_keepnan(float x) { return __builtin_elementwise_maximum(x, 0.f); }")
+PD6 = ("  constexpr int KSA = G::KSA, PD = G::PD, CB = G::CB, CP = G::CP, P = Q::P;",
+       "  constexpr int KSA = G::KSA, PD = 6, CB = G::CB, CP = G::CP, P = Q::P;")
+PD3 = ("  constexpr int KSA = G::KSA, PD = G::PD, CB = G::CB, CP = G::CP, P = Q::P;",
+       "  constexpr int KSA = G::KSA, PD = 3, CB = G::CB, CP = G::CP, P = Q::P;")
+PIN56 = ("          if ((pt * KSA + s) * NT + n < (NS * WPS > 4 ? 33 : 64)) asm volatile",
+         "          if ((pt * KSA + s) * NT + n < (NS * WPS > 4 ? 33 : 56)) asm volatile")
+PIN60 = ("          if ((pt * KSA + s) * NT + n < (NS * WPS > 4 ? 33 : 64)) asm volatile",
+         "          if ((pt * KSA + s) * NT + n < (NS * WPS > 4 ? 33 : 60)) asm volatile")
+# compile-time removals (no per-k-step branches left behind; an empty asm keeps the
+# accumulators -- hence the MFMAs -- alive at no cost)
+EPI2 = ("epi_step(rolec, ec, std::integral_constant<int, 1 - PAR>{});",
+        "sink(std::integral_constant<int, 1 - PAR>{}, ec);")
+EPI2b = ("  auto res_loads = [&](uint4 (&rvn)[G::NRF][SP], unsigned po) {",
+         "  auto sink = [&](auto pendc, auto ec) {\n"
+         "    constexpr int PQ = decltype(pendc)::value, E = decltype(ec)::value;\n"
+         "    if constexpr (E < NT) { const f32x4 t = accs[PQ][E]; asm volatile(\"\" :: \"a\"(t)); }\n"
+         "  };\n"
+         "  auto res_loads = [&](uint4 (&rvn)[G::NRF][SP], unsigned po) {")
+RES2 = ("      if constexpr (ISB && S == 0) res_loads(rvs[PAR], cur.pix);", "")
+DMA2 = ("""        dma(widx ? roff[rb] : roff[ra], widx ? rslot[rb] : rslot[ra], std::integral_constant<int, pa>{},
+            std::integral_constant<int, pb>{}, rr < nnew);""", "        (void)rr;")
+WALK2 = ("      if constexpr (S == KW) walk_adv(wk);", "")
+GEO2 = ("      if constexpr (S == KG) nxt = geo(wk);", "      if constexpr (S == KG) nxt = cur;")
+NOCOK = ("    const bool cok[3] = {k.w >= sc, true, k.w + sc < W};", "    const bool cok[3] = {true, true, true};")
+NOROK = ("    const bool rok[3] = {valid && k.j >= sr, valid, valid && k.j + sr < k.n};",
+         "    const bool rok[3] = {valid, valid, valid};")
+def kwkg(kw, kg):
+    return [("  constexpr int KW = 4;                  // k-step of the walk's advance",
+             f"  constexpr int KW = {kw};"),
+            ("  constexpr int KG = KSA - 1 - PD - 1;   // k-step of the next m-tile's geometry",
+             f"  constexpr int KG = {kg};")]
+WALKT = ("        if constexpr (TBL) walk_adv_t(wk);", "        if constexpr (TBL) {}")
+GEOT = ("        if constexpr (TBL) nxt = geo_t(wk);", "        if constexpr (TBL) nxt = cur;")
+# memory-latency probes: the same accesses at L2-resident addresses / without the DMA wait
+RESL2 = ("      if constexpr (ISB && S == 0) res_loads(rvs[PAR], cur.pix);",
+         "      if constexpr (ISB && S == 0) res_loads(rvs[PAR], cur.pix & 0xFFFFu);")
+DMAL2 = ("16, (v == 0xffffu || !ok) ? 0xF0000000u : off + v, 0, 0, 0);",
+         "16, (v == 0xffffu || !ok) ? 0xF0000000u : (off & 0xFFFFu) + v, 0, 0, 0);")
+NOWAIT = ("      if constexpr (!ISB) wait_vmcnt<0>();\n      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)\n      __builtin_amdgcn_s_barrier();",
+          "      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)\n      __builtin_amdgcn_s_barrier();")
+NOSTORE = ("            __builtin_amdgcn_raw_buffer_store_b128(v4, rrs, ppix + 16 * g,",
+           f"            if ({NEVER}) __builtin_amdgcn_raw_buffer_store_b128(v4, rrs, ppix + 16 * g,")
+VARIANTS = {
+    "nogeoT": [WALKT, GEOT],
+    "mfmaT": [EPI2b, EPI2, RES2, DMA2, BAR, WALKT, GEOT],
+    "resl2": [RESL2],
+    "dmal2": [DMAL2],
+    "nowait": [NOWAIT],
+    "nostore": [NOSTORE],
+    "memL2": [RESL2, DMAL2, NOSTORE],
+    "base": [],
+    "mfma": [EPI, RES, DMA, BAR, WALK, GEO],   # MFMAs + their operand reads only
+    "noepi": [EPI, RES],
+    "nogeo": [WALK, GEO],
+    "nobar": [BAR],
+    "nodma": [DMA],
+    "max": [MAXR],
+    "pd6": [PD6],
+    "pd6mfma": [PD6, EPI, RES, DMA, BAR, WALK, GEO],
+    "pin56": [PIN56],
+    "pin60": [PIN60],
+    "maxpd6": [MAXR, PD6],
+    "mfma2": [EPI2b, EPI2, RES2, DMA2, BAR, WALK2, GEO2],
+    "mfma2pd6": [PD6, EPI2b, EPI2, RES2, DMA2, BAR, WALK2, GEO2],
+    "noepi2": [EPI2b, EPI2, RES2],
+    "nogeo2": [WALK2, GEO2],
+    "nocok": [NOCOK],
+    "novalid": [NOCOK, NOROK],
+    "kg6": kwkg(3, 6),
+    "kg3": kwkg(1, 3),
+    "kg8": kwkg(4, 8),
+}
+
+
+def build(name, patches=None):
+    d = os.path.join(OUT, name)
+    src = os.path.join(d, "src")
+    shutil.rmtree(d, ignore_errors=True)
+    os.makedirs(d)
+    shutil.copytree(os.path.join(ROOT, "honk_amd", "csrc"), os.path.join(src, "honk_amd", "csrc"))
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(src, "include"))
+    csrc = os.path.join(src, "honk_amd", "csrc")
+    f = os.path.join(csrc, "res.hip")
+    s = open(f).read()
+    for a, b in REDUCE:
+        assert a in s, ("reduce", a[:80])
+        s = s.replace(a, b)
+    open(f, "w").write(s)
+    for pt in (patches if patches is not None else VARIANTS[name]):
+        fn, a, b = pt if len(pt) == 3 else ("res_bf16p.inc",) + tuple(pt)
+        f = os.path.join(csrc, fn)
+        s = open(f).read()
+        assert a in s, (name, fn, a[:80])
+        s = s.replace(a, b)
+        open(f, "w").write(s)
+    f = os.path.join(csrc, "res_bf16p.inc")
+    obj = os.path.join(d, "res.o")
+    cc = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-function",
+          "-save-temps=obj", "-I", os.path.join(src, "include")]
+    subprocess.run(cc + ["-c", f.replace("res_bf16p.inc", "res.hip"), "-o", obj], check=True)
+    bd = os.path.join(ROOT, "honk_amd", "_build")
+    others = [os.path.join(bd, x + ".o") for x in ("runtime", "cnn", "train", "mfcc", "head", "augment")]
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                    os.path.join(d, "libhonk_hip.so"), obj] + others, check=True)
+    shutil.rmtree(src)
+    for t in glob.glob(os.path.join(d, "*")):
+        if not t.endswith((".so", "-gfx950.s")):
+            os.remove(t)
+    return name
+
+
+RUN = r'''
+import os, sys, torch
+sys.path.insert(0, os.getcwd())
+from honk_amd import model as hm
+torch.manual_seed(0)
+m = hm.find_model("res15")(dict(hm.find_config("res15"))).eval().cuda()
+m.honk_precision, m.honk_reroute = "f16x2", False
+x = torch.randn(8192, 101, 40, device="cuda")
+with torch.no_grad():
+    for _ in range(3):
+        m(x)
+torch.cuda.synchronize()
+'''
+
+
+def time_variants(names):
+    import csv
+    for name in names:
+        lib = os.path.join(OUT, name, "libhonk_hip.so")
+        od = os.path.join(ROOT, "gpurun_out", "pair", name)
+        os.makedirs(od, exist_ok=True)
+        env = dict(os.environ, HONK_LIB=lib)
+        r = subprocess.run(["timeout", "-k", "10", "120", "rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", od, "-o", "run",
+                            "--", sys.executable, "-c", RUN], env=env, capture_output=True, text=True)
+        if r.returncode != 0:
+            print(name, "FAILED", r.returncode, r.stderr[-1500:], flush=True)
+            sys.exit(r.returncode)
+        stats = glob.glob(os.path.join(od, "**", "*kernel_stats.csv"), recursive=True)
+        row = {}
+        with open(stats[0]) as fh:
+            for rec in csv.DictReader(fh):
+                k = rec["Name"]
+                for tag in ("block16p_kernel", "block16l_kernel", "conv0m_kernel"):
+                    if tag in k:
+                        row[tag] = round(float(rec["AverageNs"]) / 1e3, 1)
+        print(f"{name:12s} " + "  ".join(f"{k} {v} us" for k, v in sorted(row.items())), flush=True)
+
+
+if __name__ == "__main__":
+    cmd, names = sys.argv[1], sys.argv[2:] or list(VARIANTS)
+    if cmd == "build":
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(min(len(names), 6)) as ex:
+            for n in ex.map(build, names):
+                print("built", n, flush=True)
+    else:
+        time_variants(names)

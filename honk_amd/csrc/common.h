@@ -44,9 +44,11 @@ inline int fail(int code, const char* fmt, ...) {
   } while (0)
 
 // ReLU with torch.relu's NaN behaviour: x <= 0 (either zero included) -> +0,
-// otherwise x -- a NaN of either sign passes (v_cmp + v_cndmask; fmaxf(x, 0) and an
-// integer max on the bits would turn a NaN, resp. a -NaN, into 0)
-__device__ __forceinline__ float relu_keepnan(float x) { return x <= 0.f ? 0.f : x; }
+// otherwise x -- a NaN of either sign stays a NaN.  IEEE 754-2019 maximum(x, +0)
+// (gfx950's v_maximum3_f32: one VALU; -0 < +0 and a NaN operand gives a NaN) -- fmaxf
+// (maxNum) and an integer max on the bits would turn a NaN, resp. a -NaN, into 0, and a
+// compare + select costs two VALU.
+__device__ __forceinline__ float relu_keepnan(float x) { return __builtin_elementwise_maximum(x, 0.f); }
 
 // sum over the 16 lanes of a row (lane group) by DPP: quad_perm [1,0,3,2], [2,3,0,1],
 // row_half_mirror, row_mirror -- after each step the lanes of the combined span hold

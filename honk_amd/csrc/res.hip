@@ -1163,8 +1163,9 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
 // Fused pair plan (res_bf16p.inc) for layers A (dilation d) and B (tap stride sB
 // class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
-static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw, int nstreams = 1) {
+static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int nstreams = 1) {
   PairPlan pp{false, 0, 0, 0, 0, 0, 0, nstreams};
+  const int SP = sp_of(FM);
   const int P = 64, W = L.W, H = L.H;
   const long PXB = g16p_pxb(L.NT, SP);  // LDS pixel pitch
   pp.ppr = (int)((W * PXB + 1023) / 1024);
@@ -1227,7 +1228,7 @@ static PairPlan plan_pair(const Layout& L, int SP, int d, int sB, int cpw, int n
   if (F(-1) < 0) return pp;
   pp.NRA = (int)(nra > 2 ? nra : 2);
   pp.NRB = (int)(nrb > 2 ? nrb : 2);
-  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + 256 + 1024 <= g16p_lds_bytes() / nstreams;
+  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + g16p_lds_extra(FM, 4) <= g16p_lds_bytes() / nstreams;
   return pp;
 }
 
@@ -1254,10 +1255,10 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
   // bf16 with full 40-pixel rows: two streams per workgroup when both rings fit half the LDS
   const char* nse = getenv("HONK_PAIR_STREAMS");
   if (FM == 0 && !(nse && nse[0] == '1')) {
-    const PairPlan p2 = plan_pair(L, SP, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2);
+    const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2);
     if (p2.ok && p2.ppr == 4 && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
   }
-  const PairPlan pp = plan_pair(L, SP, dA, sB, (int)cdiv(n, grid));
+  const PairPlan pp = plan_pair(L, FM, dA, sB, (int)cdiv(n, grid));
   const int ppw = pair_ppw(SP, pp.ppr);
   return pp.ok && ppw && pp.ppw <= ppw ? pp : no;
 }
@@ -1278,12 +1279,12 @@ static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) 
   // two streams of 2 A waves: one wave per SIMD (bf16 with four streams, two waves per
   // SIMD at 256 registers, spilled the weights: 3.38 vs 1.65 ms per 4096-clip launch)
   const int ns = 2;
-  PairPlan pp = plan_pair(L, SP, dil_of(d, i), 1, 1, ns);
+  PairPlan pp = plan_pair(L, FM, dil_of(d, i), 1, 1, ns);
   if (pp.NRA < 2 || pp.ppr != (SP == 2 ? 9 : 4) || pp.ppw > pair_ppw(SP, pp.ppr)) return no;
   pp.NRB = 1;
   pp.lag = 0;
   pp.ns = ns;
-  pp.ok = (long)(pp.NRA + 1) * pp.slotb + 256 + 1024 <= g16p_lds_bytes() / ns;
+  pp.ok = (long)(pp.NRA + 1) * pp.slotb + g16p_lds_extra(FM, 2) <= g16p_lds_bytes() / ns;
   return pp.ok ? pp : no;
 }
 
