@@ -109,8 +109,11 @@ def kwkg(kw, kg):
              f"  constexpr int KW = {kw};"),
             ("  constexpr int KG = KSA - 1 - PD - 1;   // k-step of the next m-tile's geometry",
              f"  constexpr int KG = {kg};")]
-WALKT = ("        if constexpr (TBL) walk_adv_t(wk);", "        if constexpr (TBL) {}")
-GEOT = ("        if constexpr (TBL) nxt = geo_t(wk);", "        if constexpr (TBL) nxt = cur;")
+BALON = ("  constexpr bool BAL = false;", "  constexpr bool BAL = true;")
+NOEPIA = ("          if constexpr ((KE + E < KSA ? KE + E : KSA - 1) == S) epi_step(rolec, ec, std::integral_constant<int, 1 - PAR>{});",
+          "          if constexpr ((KE + E < KSA ? KE + E : KSA - 1) == S && decltype(rolec)::value) epi_step(rolec, ec, std::integral_constant<int, 1 - PAR>{});")
+WALKT = ("        if constexpr (S == KW) walk_adv_t(wk);", "")
+GEOT = ("        if constexpr (S == KG) nxt = geo_t(wk);", "        if constexpr (S == KG) nxt = cur;")
 # memory-latency probes: the same accesses at L2-resident addresses / without the DMA wait
 RESL2 = ("      if constexpr (ISB && S == 0) res_loads(rvs[PAR], cur.pix);",
          "      if constexpr (ISB && S == 0) res_loads(rvs[PAR], cur.pix & 0xFFFFu);")
@@ -120,8 +123,50 @@ NOWAIT = ("      if constexpr (!ISB) wait_vmcnt<0>();\n      __builtin_amdgcn_s_
           "      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)\n      __builtin_amdgcn_s_barrier();")
 NOSTORE = ("            __builtin_amdgcn_raw_buffer_store_b128(v4, rrs, ppix + 16 * g,",
            f"            if ({NEVER}) __builtin_amdgcn_raw_buffer_store_b128(v4, rrs, ppix + 16 * g,")
+# in-kernel stamps (diagnostic build): per wave, cycles in the step loop, at the DMA wait,
+# at the barrier; read back through honk_dbg_read
+STAMP = [
+    ("  float* chsum;         // last-layer mode: [nclips][2][CP] channel sums of relu(A's output)\n};",
+     "  float* chsum;         // last-layer mode: [nclips][2][CP] channel sums of relu(A's output)\n  unsigned long long* dbg;\n};"),
+    ("    for (int k = 0; k < nsteps; ++k) {\n      // step barrier",
+     "    unsigned long long t_all = __builtin_amdgcn_s_memtime(), t_vm = 0, t_bar = 0;\n    for (int k = 0; k < nsteps; ++k) {\n      // step barrier"),
+    ("      asm volatile(\"\" ::: \"memory\");\n      if constexpr (!ISB) wait_vmcnt<0>();",
+     "      asm volatile(\"\" ::: \"memory\");\n      const unsigned long long ta = __builtin_amdgcn_s_memtime();\n      if constexpr (!ISB) wait_vmcnt<0>();"),
+    ("      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)\n      __builtin_amdgcn_s_barrier();\n      asm volatile(\"\" ::: \"memory\");\n      if constexpr (TBL) {",
+     "      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)\n      const unsigned long long tb = __builtin_amdgcn_s_memtime();\n      __builtin_amdgcn_s_barrier();\n      const unsigned long long tc = __builtin_amdgcn_s_memtime();\n      t_vm += tb - ta;\n      t_bar += tc - tb;\n      asm volatile(\"\" ::: \"memory\");\n      if constexpr (TBL) {"),
+    ("    wait_vmcnt<0>();\n    static_for<ELAST + 1>([&](auto ec) { epi_step(rolec, ec, std::integral_constant<int, 1>{}); });",
+     "    wait_vmcnt<0>();\n    static_for<ELAST + 1>([&](auto ec) { epi_step(rolec, ec, std::integral_constant<int, 1>{}); });\n"
+     "    t_all = __builtin_amdgcn_s_memtime() - t_all;\n"
+     "    if (!LM && a.dbg && lane == 0) {\n"
+     "      unsigned long long* o = a.dbg + ((size_t)blockIdx.x * 8 + wave) * 4;\n"
+     "      o[0] = t_all; o[1] = t_vm; o[2] = t_bar; o[3] = (unsigned long long)nsteps;\n    }"),
+    ("res.hip", "            pa.chsum = nullptr;", "            pa.chsum = nullptr;\n            pa.dbg = honk_dbg_buf();"),
+    ("res.hip", "            pa.chsum = chsum;", "            pa.chsum = chsum;\n            pa.dbg = nullptr;"),
+    ("res.hip", "struct PairPlan {", "static unsigned long long* honk_dbg_buf() {\n  static unsigned long long* b = nullptr;\n"
+     "  if (!b) { (void)hipMalloc(&b, 1 << 20); (void)hipMemset(b, 0, 1 << 20); }\n  return b;\n}\nstruct PairPlan {"),
+    ("res.hip", "extern \"C\" {", "extern \"C\" {\n"
+     "int honk_dbg_read(unsigned long long* h, int n) { (void)hipDeviceSynchronize(); return (int)hipMemcpy(h, honk::res::honk_dbg_buf(), n * 8, hipMemcpyDeviceToHost); }"),
+]
 VARIANTS = {
+    "stamp": STAMP,
+    "stampdmaA": STAMP + [("  constexpr bool DMAB = !LM;", "  constexpr bool DMAB = false;")],
+    "stampnogeo": STAMP + [WALKT, GEOT],
+    "stampnodma": STAMP + [DMA2],
+    "stampmfma": STAMP + [EPI2b, EPI2, RES2, DMA2, WALKT, GEOT],
     "nogeoT": [WALKT, GEOT],
+    "bal": [BALON],
+    "dmaA": [("  constexpr bool DMAB = !LM;", "  constexpr bool DMAB = false;")],
+    "pd1": [("  constexpr int PD = (FM == 2 && KSA % 7 == 0) ? 6 : G::PD;", "  constexpr int PD = G::PD;")],
+    "noB": [("    if (role == 0) run_role(std::integral_constant<bool, false>{});\n    else run_role(std::integral_constant<bool, true>{});",
+             "    if (role == 0) run_role(std::integral_constant<bool, false>{});\n    else for (int k = 0; k < nsteps; ++k) __builtin_amdgcn_s_barrier();")],
+    "noA": [("    if (role == 0) run_role(std::integral_constant<bool, false>{});\n    else run_role(std::integral_constant<bool, true>{});",
+             "    if (role == 0) { for (int k = 0; k < nsteps; ++k) __builtin_amdgcn_s_barrier(); }\n    else run_role(std::integral_constant<bool, true>{});")],
+    "nomix": [("res_bf16w.inc", "  if constexpr (FM == 2) {\n    float out;", "  if constexpr (FM == 22) {\n    float out;")],
+    "balpd6": [BALON, PD6],
+    "nodma": [DMA2],
+    "nobar": [BAR],
+    "noslp": [("CFLAGS", "-fno-slp-vectorize", "")],
+    "noepiA": [NOEPIA],
     "mfmaT": [EPI2b, EPI2, RES2, DMA2, BAR, WALKT, GEOT],
     "resl2": [RESL2],
     "dmal2": [DMAL2],
@@ -166,8 +211,12 @@ def build(name, patches=None):
         assert a in s, ("reduce", a[:80])
         s = s.replace(a, b)
     open(f, "w").write(s)
+    cflags = []
     for pt in (patches if patches is not None else VARIANTS[name]):
         fn, a, b = pt if len(pt) == 3 else ("res_bf16p.inc",) + tuple(pt)
+        if fn == "CFLAGS":
+            cflags.append(a)
+            continue
         f = os.path.join(csrc, fn)
         s = open(f).read()
         assert a in s, (name, fn, a[:80])
@@ -177,7 +226,7 @@ def build(name, patches=None):
     obj = os.path.join(d, "res.o")
     cc = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-function",
           "-save-temps=obj", "-I", os.path.join(src, "include")]
-    subprocess.run(cc + ["-c", f.replace("res_bf16p.inc", "res.hip"), "-o", obj], check=True)
+    subprocess.run(cc + cflags + ["-c", f.replace("res_bf16p.inc", "res.hip"), "-o", obj], check=True)
     bd = os.path.join(ROOT, "honk_amd", "_build")
     others = [os.path.join(bd, x + ".o") for x in ("runtime", "cnn", "train", "mfcc", "head", "augment")]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
@@ -227,6 +276,57 @@ def time_variants(names):
         print(f"{name:12s} " + "  ".join(f"{k} {v} us" for k, v in sorted(row.items())), flush=True)
 
 
+RUNSTAMP = RUN + r'''
+import ctypes, numpy as np
+lib = ctypes.CDLL(os.environ["HONK_LIB"])
+buf = np.zeros(256 * 8 * 4, dtype=np.uint64)
+lib.honk_dbg_read(buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+b = buf.reshape(256, 8, 4).astype(np.float64)
+for role, ws in (("A", [0, 1]), ("B", [2, 3])):
+    t = b[:, ws, :]
+    print(f"{role}: loop {np.median(t[..., 0]) / 1e3:.1f}K cyc  dma-wait {np.median(t[..., 1]) / 1e3:.1f}K  barrier {np.median(t[..., 2]) / 1e3:.1f}K"
+          f"  steps {np.median(t[..., 3]):.0f}  per step {np.median(t[..., 0] / t[..., 3]):.0f} cyc"
+          f" (wait {np.median(t[..., 1] / t[..., 3]):.0f}, bar {np.median(t[..., 2] / t[..., 3]):.0f})")
+'''
+
+
+def stamp_run(name):
+    lib = os.path.join(OUT, name, "libhonk_hip.so")
+    env = dict(os.environ, HONK_LIB=lib)
+    r = subprocess.run(["timeout", "-k", "10", "120", sys.executable, "-c", RUNSTAMP], env=env, capture_output=True, text=True)
+    print(name, r.returncode, r.stdout[-3000:], r.stderr[-2000:] if r.returncode else "", flush=True)
+
+
+PMC = "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
+
+
+def pmc_variants(names):
+    """one --pmc pass per variant (kernel-trace only beside it): per-launch means of the pair kernel"""
+    import csv
+    from collections import defaultdict
+    for name in names:
+        lib = os.path.join(OUT, name, "libhonk_hip.so")
+        od = os.path.join(ROOT, "gpurun_out", "pairpmc", name)
+        os.makedirs(od, exist_ok=True)
+        env = dict(os.environ, HONK_LIB=lib)
+        r = subprocess.run(["timeout", "-s", "KILL", "90", "rocprofv3", "--pmc"] + PMC.split() +
+                           ["--output-format", "csv", "-d", od, "-o", "run", "--", sys.executable, "-c", RUN],
+                           env=env, capture_output=True, text=True)
+        if r.returncode != 0:
+            print(name, "FAILED", r.returncode, r.stderr[-1500:], flush=True)
+            sys.exit(r.returncode)
+        f = glob.glob(os.path.join(od, "**", "*counter_collection.csv"), recursive=True)[0]
+        acc = defaultdict(lambda: defaultdict(list))
+        with open(f) as fh:
+            for rec in csv.DictReader(fh):
+                for tag in ("block16p_kernel", "block16l_kernel"):
+                    if tag in rec["Kernel_Name"]:
+                        acc[tag][rec["Counter_Name"]].append(float(rec["Counter_Value"]))
+        for tag, cs in acc.items():
+            m = {k: sum(v) / len(v) for k, v in cs.items()}
+            print(f"{name:10s} {tag}: " + " ".join(f"{k.replace('SQ_', '')}={v:.4g}" for k, v in sorted(m.items())), flush=True)
+
+
 if __name__ == "__main__":
     cmd, names = sys.argv[1], sys.argv[2:] or list(VARIANTS)
     if cmd == "build":
@@ -234,5 +334,10 @@ if __name__ == "__main__":
         with ThreadPoolExecutor(min(len(names), 6)) as ex:
             for n in ex.map(build, names):
                 print("built", n, flush=True)
+    elif cmd == "stamp":
+        for n in names:
+            stamp_run(n)
+    elif cmd == "pmc":
+        pmc_variants(names)
     else:
         time_variants(names)

@@ -1228,7 +1228,7 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   if (F(-1) < 0) return pp;
   pp.NRA = (int)(nra > 2 ? nra : 2);
   pp.NRB = (int)(nrb > 2 ? nrb : 2);
-  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + g16p_lds_extra(FM, 4) <= g16p_lds_bytes() / nstreams;
+  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + g16p_lds_extra(FM, 4, pp.slotb) <= g16p_lds_bytes() / nstreams;
   return pp;
 }
 
@@ -1284,7 +1284,7 @@ static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) 
   pp.NRB = 1;
   pp.lag = 0;
   pp.ns = ns;
-  pp.ok = (long)(pp.NRA + 1) * pp.slotb + g16p_lds_extra(FM, 2) <= g16p_lds_bytes() / ns;
+  pp.ok = (long)(pp.NRA + 1) * pp.slotb + g16p_lds_extra(FM, 2, pp.slotb) <= g16p_lds_bytes() / ns;
   return pp.ok ? pp : no;
 }
 
