@@ -1,3 +1,3 @@
 mkdir -p gpurun_out && export TMPDIR=/tmp && \
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5q_pytest.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/r5q_bench.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5r_pytest.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/r5r_bench.log 2>&1

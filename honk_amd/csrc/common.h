@@ -55,10 +55,14 @@ __device__ __forceinline__ float relu_keepnan(float x) { return __builtin_elemen
 // the same value (IEEE addition is commutative), so every lane of the row returns the
 // row's sum; VALU only (a __shfl_xor tree goes through the LDS crossbar)
 __device__ __forceinline__ float sum16_dpp(float t) {
-  t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0xB1, 0xF, 0xF, false));
-  t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0x4E, 0xF, 0xF, false));
-  t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0x141, 0xF, 0xF, false));
-  t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0x140, 0xF, 0xF, false));
+  // (mov_dpp with bound_ctrl: every source lane of these patterns exists, and the
+  // combiner then folds each step into one v_add_f32 with a DPP operand -- update_dpp's
+  // explicit old value kept a separate v_mov_b32_dpp and a temporary per step, which
+  // spilled the row-band kernel's last layer: 102 vs 65 us per res8 launch)
+  t += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0xB1, 0xF, 0xF, true));
+  t += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0x4E, 0xF, 0xF, true));
+  t += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0x141, 0xF, 0xF, true));
+  t += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0x140, 0xF, 0xF, true));
   return t;
 }
 

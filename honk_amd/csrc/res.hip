@@ -1669,7 +1669,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       }
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
-                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * 8, L.H * L.W, L.C, L.CP, L.NL,
+                         packed + L.off_bout, logits + c0 * L.NL, nbc_last * 8 * pr.MT, L.H * L.W, L.C, L.CP, L.NL,
                          bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16 row-band)");
     }
@@ -1760,7 +1760,7 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
       return 0;
     }
     const int nb = max_bands_per_clip(L, pr.TH, d->use_dilation);
-    size_t parts = (size_t)nb * 8;  // row-band kernel: [tile][wave] channel sums
+    size_t parts = (size_t)nb * 8 * pr.MT;  // row-band kernel: [tile][wave][m-tile] channel sums
     if (wpath) {
       const size_t pw = (size_t)bands_w(L, d, FM, L.L) * 4;  // weight-stationary: [tile][wave]
       if (pw > parts) parts = pw;
