@@ -26,6 +26,9 @@ VARIANTS = {
     "c0nostore": [("res.hip", "    if (q0 >= npo) continue;\n    char* op = oc + (size_t)q0 * CB;",
                    "    if (q0 >= npo || clip >= 0) { for (int n = 0; n < NT; ++n) asm volatile(\"\" :: \"v\"(pacc[n])); continue; }\n    char* op = oc + (size_t)q0 * CB;")],
     "pairw": [],
+    "net": [],
+    "net15": [("CFLAGS", "-DHONK_NET_ABL=15", "")],
+    "net7": [("CFLAGS", "-DHONK_NET_ABL=7", "")],
     "pairB": [("res.hip", "(FM == 1 || (L.W >= 32 && L.L >= 3 &&", "(FM == 1 || (L.W >= 8 && L.L >= 3 &&")],
     "pairT": [("res_bf16p.inc", "  constexpr bool TBL = FM == 2;", "  constexpr bool TBL = FM == 2 || (FM == 0 && NS == 1);"),
               ("res_bf16p.inc", "  constexpr int PD = (FM == 2 && KSA % 7 == 0) ? 6 : G::PD;",
@@ -45,7 +48,11 @@ def build(name):
     shutil.copytree(os.path.join(ROOT, "honk_amd", "csrc"), os.path.join(src, "honk_amd", "csrc"))
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(src, "include"))
     csrc = os.path.join(src, "honk_amd", "csrc")
+    cflags = []
     for fn, a, b in VARIANTS[name]:
+        if fn == "CFLAGS":
+            cflags.append(a)
+            continue
         f = os.path.join(csrc, fn)
         s = open(f).read()
         assert a in s, (name, fn, a[:80])
@@ -53,7 +60,7 @@ def build(name):
     obj = os.path.join(d, "res.o")
     cc = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-function",
           "-I", os.path.join(src, "include")]
-    subprocess.run(cc + ["-c", os.path.join(csrc, "res.hip"), "-o", obj], check=True)
+    subprocess.run(cc + cflags + ["-c", os.path.join(csrc, "res.hip"), "-o", obj], check=True)
     bd = os.path.join(ROOT, "honk_amd", "_build")
     others = [os.path.join(bd, x + ".o") for x in ("runtime", "cnn", "train", "mfcc", "head", "augment")]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
@@ -66,14 +73,15 @@ def build(name):
 RUN = os.path.join(ROOT, "exp", "c3_prof.py")
 
 
-ENV = {"pairw": {"HONK_RES_KERNEL": "w"}}
+ENV = {"pairw": {"HONK_RES_KERNEL": "w"}, "net": {"HONK_RES_KERNEL": "n"}, "net15": {"HONK_RES_KERNEL": "n"},
+       "net7": {"HONK_RES_KERNEL": "n"}}
 
 
 def time_variants(names):
     for name in names:
         od = os.path.join(ROOT, "gpurun_out", "c3", name)
         os.makedirs(od, exist_ok=True)
-        env = dict(os.environ, HONK_LIB=os.path.join(OUT, name if name != "pairw" else "base", "libhonk_hip.so"),
+        env = dict(os.environ, HONK_LIB=os.path.join(OUT, name if name not in ("pairw", "net") else "base", "libhonk_hip.so"),
                    **ENV.get(name, {}))
         r = subprocess.run(["timeout", "-k", "10", "120", "rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv",
                             "-d", od, "-o", "run", "--", sys.executable, RUN], env=env, capture_output=True, text=True)
