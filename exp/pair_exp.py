@@ -155,6 +155,10 @@ VARIANTS = {
     "stampmfma": STAMP + [EPI2b, EPI2, RES2, DMA2, WALKT, GEOT],
     "nogeoT": [WALKT, GEOT],
     "bal": [BALON],
+    "pin60": [PIN60],
+    "pin56": [PIN56],
+    "pin48": [("          if ((pt * KSA + s) * NT + n < (NS * WPS > 4 ? 33 : 64)) asm volatile",
+               "          if ((pt * KSA + s) * NT + n < (NS * WPS > 4 ? 33 : 48)) asm volatile")],
     "dmaA": [("  constexpr bool DMAB = !LM;", "  constexpr bool DMAB = false;")],
     "pd1": [("  constexpr int PD = (FM == 2 && KSA % 7 == 0) ? 6 : G::PD;", "  constexpr int PD = G::PD;")],
     "noB": [("    if (role == 0) run_role(std::integral_constant<bool, false>{});\n    else run_role(std::integral_constant<bool, true>{});",
