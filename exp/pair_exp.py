@@ -155,6 +155,9 @@ VARIANTS = {
     "stampmfma": STAMP + [EPI2b, EPI2, RES2, DMA2, WALKT, GEOT],
     "nogeoT": [WALKT, GEOT],
     "bal": [BALON],
+    "dsp2": [("  constexpr int DSP = 1;", "  constexpr int DSP = 2;")],
+    "dsp3": [("  constexpr int DSP = 1;", "  constexpr int DSP = 3;")],
+    "dsp4": [("  constexpr int DSP = 1;", "  constexpr int DSP = 4;")],
     "pin60": [PIN60],
     "pin56": [PIN56],
     "pin48": [("          if ((pt * KSA + s) * NT + n < (NS * WPS > 4 ? 33 : 64)) asm volatile",

@@ -1138,6 +1138,7 @@ static int bands_w(const Layout& L, const honk_res_desc* d, int FM, int i) {
 struct PairPlan {
   bool ok;
   int lag, NRA, NRB, slotb, ppr, ppw;  // ppw: DMA pieces per A wave per step
+  int padb;                            // f16x2: zero-column bytes each side of a slot's row
   int ns;                              // streams per workgroup (block16p_kernel NS)
 };
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i);
@@ -1163,8 +1164,8 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
 // Fused pair plan (res_bf16p.inc) for layers A (dilation d) and B (tap stride sB
 // class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
-static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int nstreams = 1) {
-  PairPlan pp{false, 0, 0, 0, 0, 0, 0, nstreams};
+static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int nstreams = 1, bool padcols = false) {
+  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams};
   const int SP = sp_of(FM);
   const int P = 64, W = L.W, H = L.H;
   const long PXB = g16p_pxb(L.NT, SP);  // LDS pixel pitch
@@ -1172,6 +1173,15 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   // slot pitch: room for the DMA's whole pieces, = W * PXB mod 256 so that
   // stream pixels stay at a constant LDS pitch across a row change
   pp.slotb = (int)(W * PXB + ((pp.ppr * 1024 - W * PXB + 255) / 256) * 256);
+  if (FM == 2 && padcols) {
+    // f16x2 last layer (res_bf16p.inc PADC): zero columns either side of every slot's
+    // row, at least the widest tap offset (B's sB d columns), in 256-B units; the DMA's
+    // pieces and their zero tail after the left pad
+    const long sc = (long)sB * d;
+    pp.padb = (int)((sc * PXB + 255) / 256 * 256);
+    const long right = W * PXB + pp.padb > pp.ppr * 1024L ? W * PXB + pp.padb : pp.ppr * 1024L;
+    pp.slotb = (int)((pp.padb + right + 255) / 256 * 256);
+  }
   const long total = (long)cpw * H * W, rows_total = (long)cpw * H;
   if (total >= (1L << 24) || sB < 1 || sB > 2) return pp;
   auto rho = [&](long q) { return q / W; };
@@ -1243,7 +1253,7 @@ static int pair_ppw(int SP, int ppr) {
   return ppr == 4 ? 4 : ppr == 2 ? 5 : 0;
 }
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i) {
-  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 1};
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1};
   const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
@@ -1270,7 +1280,7 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
 // (no A-out ring: NRB = 1 unused slot, no lag).  HONK_LAST_KERNEL=w keeps the
 // weight-stationary kernel (the pair-vs-w bitwise tests).
 static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) {
-  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 1};
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1};
   const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   const char* lenv = getenv("HONK_LAST_KERNEL");
@@ -1279,7 +1289,7 @@ static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) 
   // two streams of 2 A waves: one wave per SIMD (bf16 with four streams, two waves per
   // SIMD at 256 registers, spilled the weights: 3.38 vs 1.65 ms per 4096-clip launch)
   const int ns = 2;
-  PairPlan pp = plan_pair(L, FM, dil_of(d, i), 1, 1, ns);
+  PairPlan pp = plan_pair(L, FM, dil_of(d, i), 1, 1, ns, true);
   if (pp.NRA < 2 || pp.ppr != (SP == 2 ? 9 : 4) || pp.ppw > pair_ppw(SP, pp.ppr)) return no;
   pp.NRB = 1;
   pp.lag = 0;
@@ -1554,6 +1564,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.NRB = pp.NRB;
             pa.slotb = pp.slotb;
             pa.ppr = pp.ppr;
+            pa.padb = pp.padb;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(256 * pp.ns);
             if (FM == 1 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9, 1>), gd, bd, 0, st, pa);
@@ -1587,6 +1598,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.NRB = lp.NRB;
             pa.slotb = lp.slotb;
             pa.ppr = lp.ppr;
+            pa.padb = lp.padb;
             pa.chsum = chsum;
             TimedLaunch tl(st, layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(128 * lp.ns);
