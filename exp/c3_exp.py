@@ -26,6 +26,8 @@ VARIANTS = {
     "c0nostore": [("res.hip", "    if (q0 >= npo) continue;\n    char* op = oc + (size_t)q0 * CB;",
                    "    if (q0 >= npo || clip >= 0) { for (int n = 0; n < NT; ++n) asm volatile(\"\" :: \"v\"(pacc[n])); continue; }\n    char* op = oc + (size_t)q0 * CB;")],
     "pairw": [],
+    "c0lb8": [("res.hip", "__global__ __launch_bounds__(256) void conv0m_kernel(", "__global__ __launch_bounds__(256, 8) void conv0m_kernel(")],
+    "c0lb7": [("res.hip", "__global__ __launch_bounds__(256) void conv0m_kernel(", "__global__ __launch_bounds__(256, 7) void conv0m_kernel(")],
     "net": [],
     "net15": [("CFLAGS", "-DHONK_NET_ABL=15", "")],
     "net7": [("CFLAGS", "-DHONK_NET_ABL=7", "")],

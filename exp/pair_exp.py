@@ -149,12 +149,30 @@ STAMP = [
 ]
 VARIANTS = {
     "stamp": STAMP,
+    "stampsametq": STAMP + [("        if constexpr (S == KG) nxt = geo_t(wk);",
+                 "        if constexpr (S == KG) { const MG g2 = geo_t(wk); nxt = cur; nxt.pix = g2.pix; nxt.lo = g2.lo; }")],
     "stampdmaA": STAMP + [("  constexpr bool DMAB = !LM;", "  constexpr bool DMAB = false;")],
     "stampnogeo": STAMP + [WALKT, GEOT],
     "stampnodma": STAMP + [DMA2],
     "stampmfma": STAMP + [EPI2b, EPI2, RES2, DMA2, WALKT, GEOT],
     "nogeoT": [WALKT, GEOT],
     "bal": [BALON],
+    # which part of the geometry costs: the table read, the tap addresses, the pixel addresses
+    "gnoread": [("    k.e = *(const u32x4*)e;\n    k.lo = *(const int*)(e + 16);",
+                 "    k.e = u32x4{(unsigned)(k.r & 1) * 4096u + (unsigned)ringA, (unsigned)ringA + 4096u, (unsigned)ringA + 8192u, (unsigned)(k.r * 3840)};\n    k.lo = ringB + (k.r & 3) * 4096;")],
+    "gnozrow": [("      if (j >= sr) rb0 = ring + ((r - sr) % nr) * a.slotb + padb;\n      if (j + sr < n) rb2 = ring + ((r + sr) % nr) * a.slotb + padb;",
+                 "      rb0 = ring + ((r + nr - sr) % nr) * a.slotb + padb;\n      rb2 = ring + ((r + sr) % nr) * a.slotb + padb;")],
+    "gnozero": [("      if (j >= sr) rb0 = ring + ((r - sr) % nr) * a.slotb + padb;\n      if (j + sr < n) rb2 = ring + ((r + sr) % nr) * a.slotb + padb;",
+                 "      rb0 = ring + ((r + nr - sr) % nr) * a.slotb + padb;\n      rb2 = ring + ((r + sr) % nr) * a.slotb + padb;"),
+                ("      for (int dx = 0; dx < 3; ++dx) m.tq[DY * 3 + dx] = ok[dx] ? rb + tk[DY * 3 + dx] : zg0;",
+                 "      for (int dx = 0; dx < 3; ++dx) m.tq[DY * 3 + dx] = rb + tk[DY * 3 + dx] - (ok[dx] ? 0 : (dx - 1) * scb);")],
+    "kw1kg3": kwkg(1, 3),
+    "kw1kg2": kwkg(1, 2),
+    "kw0kg2": kwkg(0, 2),
+    "gsametq": [("        if constexpr (S == KG) nxt = geo_t(wk);",
+                 "        if constexpr (S == KG) { const MG g2 = geo_t(wk); nxt = cur; nxt.pix = g2.pix; nxt.lo = g2.lo; }")],
+    "gsamepix": [("        if constexpr (S == KG) nxt = geo_t(wk);",
+                  "        if constexpr (S == KG) { const MG g2 = geo_t(wk); nxt = g2; nxt.pix = cur.pix; nxt.lo = cur.lo; }")],
     "dsp2": [("  constexpr int DSP = 1;", "  constexpr int DSP = 2;")],
     "dsp3": [("  constexpr int DSP = 1;", "  constexpr int DSP = 3;")],
     "dsp4": [("  constexpr int DSP = 1;", "  constexpr int DSP = 4;")],

@@ -562,7 +562,9 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 // cscale (FM 2 only, else null): the clips' power-of-two scales (clip_scale_kernel): the
 // output is s * relu(conv0(x)) (pooled) and channel C holds s instead of 1.0.
 template <int NT, int PH, int PW, int FM, bool ONES, int FWB = 0>
-__global__ __launch_bounds__(256) void conv0m_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
+// (launch bounds: 7 waves per SIMD -- 72 registers, a few 4-byte whole-tuple spills in the
+// 4x3-pool instances: res8's conv0m 114 -> 110 us per 4096 clips at 6 workgroups per CU vs 5)
+__global__ __launch_bounds__(256, 7) void conv0m_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
                                                      const float* __restrict__ w0, int Hin, int Win, int H, int W,
                                                      int C, const float* __restrict__ cscale) {
   constexpr int CP = 16 * NT, P = PH * PW, SP = FM == 1 ? 2 : 1, CB = CP * 2 * SP;
