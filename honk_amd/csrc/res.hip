@@ -504,26 +504,37 @@ __global__ __launch_bounds__(256) void tail_kernel(const float* __restrict__ x, 
 // logits[b] = Wout . (sum of the fused per-tile channel sums) / HW + bout
 // bn_scale/bn_shift: the last layer's BatchNorm applied to the channel means
 // (bf16 path, whose activations are pre-BN), or nullptr (fp32 path)
-__global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ chsum, const float* __restrict__ wout,
-                                                      const float* __restrict__ bout, float* __restrict__ logits,
-                                                      int nparts, int HW, int C, int CP, int NL,
-                                                      const float* __restrict__ bn_scale,
-                                                      const float* __restrict__ bn_shift,
-                                                      const float* __restrict__ cscale,
-                                                      const float* __restrict__ oscale) {
+__global__ __launch_bounds__(256) void tail_sum_kernel(const float* __restrict__ chsum, const float* __restrict__ wout,
+                                                       const float* __restrict__ bout, float* __restrict__ logits,
+                                                       int nparts, int HW, int C, int CP, int NL,
+                                                       const float* __restrict__ bn_scale,
+                                                       const float* __restrict__ bn_shift,
+                                                       const float* __restrict__ cscale,
+                                                       const float* __restrict__ oscale) {
+  // groups of 64 threads sum every ng-th partial (coalesced rows of CP floats), then one
+  // thread per channel adds the groups' sums in group order: a fixed order for every clip
+  // (the row-band last layer writes 8 waves x MT m-tiles x bands partials per clip; one
+  // thread walking all of them serially took 15 us per 4096-clip chunk)
+  __shared__ float part[4][64];
   __shared__ float mean[64];
   const int b = blockIdx.x;
-  const int c = threadIdx.x;
+  const int t = threadIdx.x, c = t & 63, grp = t >> 6, ng = blockDim.x >> 6;
+  float s = 0.f;
   if (c < CP) {
     const float* p = chsum + (size_t)b * nparts * CP + c;
-    float s = 0.f;
-    for (int i = 0; i < nparts; ++i) s += p[(size_t)i * CP];
+    for (int i = grp; i < nparts; i += ng) s += p[(size_t)i * CP];
+  }
+  part[grp][c] = s;
+  __syncthreads();
+  if (t < CP) {
+    float v = part[0][t];
+    for (int g = 1; g < ng; ++g) v += part[g][t];
     // the f16x2 clip scale times the last layer's output exponent (powers of two: exact)
-    if (cscale) s /= cscale[b] * *oscale;
-    mean[c] = bn_scale ? fmaf(s / (float)HW, bn_scale[c], bn_shift[c]) : s / (float)HW;
+    if (cscale) v /= cscale[b] * *oscale;
+    mean[t] = bn_scale ? fmaf(v / (float)HW, bn_scale[t], bn_shift[t]) : v / (float)HW;
   }
   __syncthreads();
-  for (int n = c; n < NL; n += blockDim.x) {
+  for (int n = t; n < NL; n += blockDim.x) {
     float acc = 0.f;
     for (int k = 0; k < C; ++k) acc = fmaf(wout[n * C + k], mean[k], acc);
     logits[(int64_t)b * NL + n] = acc + bout[n];
@@ -563,7 +574,7 @@ __global__ __launch_bounds__(64) void tail_sum_kernel(const float* __restrict__ 
 // output is s * relu(conv0(x)) (pooled) and channel C holds s instead of 1.0.
 template <int NT, int PH, int PW, int FM, bool ONES, int FWB = 0>
 // (launch bounds: 7 waves per SIMD -- 72 registers, a few 4-byte whole-tuple spills in the
-// 4x3-pool instances: res8's conv0m 114 -> 110 us per 4096 clips at 6 workgroups per CU vs 5)
+// 4x3-pool instances: res8's conv0m 114 -> 110 us per 4096 clips at 7 workgroups per CU vs 6)
 __global__ __launch_bounds__(256, 7) void conv0m_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
                                                      const float* __restrict__ w0, int Hin, int Win, int H, int W,
                                                      int C, const float* __restrict__ cscale) {
@@ -1254,6 +1265,13 @@ static int pair_ppw(int SP, int ppr) {
   if (SP == 2) return ppr == 9 ? 9 : ppr == 5 ? 10 : ppr == 3 ? 9 : 0;
   return ppr == 4 ? 4 : ppr == 2 ? 5 : 0;
 }
+// f16x2 pairs with an instantiated compile-time tap step (block16p_kernel SCA / SCB: res15's
+// dilation pairs on 40-pixel rows): their rings carry pad columns (plan_pair padcols)
+static bool pair_imm(const Layout& L, int FM, int dA, int dB) {
+  if (FM != 2 || L.W != 40 || L.NT != 3) return false;
+  return (dA == 1 && (dB == 1 || dB == 2)) || (dA == 2 && dB == 2) || (dA == 4 && (dB == 4 || dB == 8)) ||
+         (dA == 8 && dB == 8);
+}
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i) {
   const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1};
   const int SP = sp_of(FM);
@@ -1270,7 +1288,7 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
     const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2);
     if (p2.ok && p2.ppr == 4 && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
   }
-  const PairPlan pp = plan_pair(L, FM, dA, sB, (int)cdiv(n, grid));
+  const PairPlan pp = plan_pair(L, FM, dA, sB, (int)cdiv(n, grid), 1, pair_imm(L, FM, dA, dB));
   const int ppw = pair_ppw(SP, pp.ppr);
   return pp.ok && ppw && pp.ppw <= ppw ? pp : no;
 }
@@ -1513,7 +1531,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       rc = L.NT == 3 ? launch_block16n<3>(L, R, frb, frl, chsum, n, st) : launch_block16n<2>(L, R, frb, frl, chsum, n, st);
       if (rc) return rc;
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
-      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, 4, L.H * L.W, L.C, L.CP, L.NL, bn_last,
                          bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (whole stack)");
@@ -1572,7 +1590,16 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             if (FM == 1 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9, 1>), gd, bd, 0, st, pa);
             else if (FM == 1 && pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10, 1>), gd, bd, 0, st, pa);
             else if (FM == 1) hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9, 1>), gd, bd, 0, st, pa);
-            else if (FM == 2 && pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1, 2>), gd, bd, 0, st, pa);
+            else if (FM == 2 && pp.ppr == 4 && pp.padb > 0) {
+              const int dB = dil_of(d, i + 1);
+#define HONK_PI(a_, b_)                                                                              \
+  else if (dA == a_ && dB == b_) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1, 2, a_, b_>), gd, bd, 0, st, pa);
+              if (false) {
+              }
+              HONK_PI(1, 1) HONK_PI(1, 2) HONK_PI(2, 2) HONK_PI(4, 4) HONK_PI(4, 8) HONK_PI(8, 8)
+#undef HONK_PI
+              else return fail(HONK_ERR_UNSUPPORTED, "block16p: no tap-step instance for dilations %d, %d", dA, dB);
+            } else if (FM == 2 && pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1, 2>), gd, bd, 0, st, pa);
             else if (FM == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 1, 2>), gd, bd, 0, st, pa);
             else if (pp.ppr == 4 && pp.ns == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
             else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1>), gd, bd, 0, st, pa);
@@ -1605,6 +1632,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             TimedLaunch tl(st, layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(128 * lp.ns);
             if (FM == 1) hipLaunchKernelGGL((block16l_kernel<3, 2, 9, 9, 2>), gd, bd, 0, st, pa);
+            else if (FM == 2 && pa.d == 16) hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2, 2, 16>), gd, bd, 0, st, pa);
             else if (FM == 2) hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2, 2>), gd, bd, 0, st, pa);
             else hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
             HONK_LAUNCH_CHECK("res block16l_kernel");
@@ -1639,7 +1667,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         if (rc) return rc;
       }
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
-      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, parts_last, L.H * L.W, L.C, L.CP, L.NL,
                          bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (weight-stationary)");
@@ -1682,7 +1710,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         if (rc) return rc;
       }
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
-      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, nbc_last * 8 * pr.MT, L.H * L.W, L.C, L.CP, L.NL,
                          bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16 row-band)");
@@ -1980,7 +2008,7 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
                          L.CP, L.NL);
       HONK_LAUNCH_CHECK("res tail_kernel");
     } else {
-      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(64), 0, st, chsum, packed + L.off_wout,
+      hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, p.nbands * MW, L.H * L.W, L.C, L.CP, L.NL,
                          (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
                          (const float*)nullptr);
