@@ -253,15 +253,20 @@ def build(name, patches=None):
         assert a in s, (name, fn, a[:80])
         s = s.replace(a, b)
         open(f, "w").write(s)
-    f = os.path.join(csrc, "res_bf16p.inc")
-    obj = os.path.join(d, "res.o")
+    sys.path.insert(0, ROOT)
+    from honk_amd.build import FLAGS
     cc = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-function",
           "-save-temps=obj", "-I", os.path.join(src, "include")]
-    subprocess.run(cc + cflags + ["-c", f.replace("res_bf16p.inc", "res.hip"), "-o", obj], check=True)
+    objs = []  # res.hip and res_f16.hip (the f16x2 pair / last layer, with their own flags)
+    procs = []
+    for tu in ("res.hip", "res_f16.hip"):
+        objs.append(os.path.join(d, tu.replace(".hip", ".o")))
+        procs.append(subprocess.Popen(cc + FLAGS.get(tu, []) + cflags + ["-c", os.path.join(csrc, tu), "-o", objs[-1]]))
+    assert all(p.wait() == 0 for p in procs), name
     bd = os.path.join(ROOT, "honk_amd", "_build")
     others = [os.path.join(bd, x + ".o") for x in ("runtime", "cnn", "train", "mfcc", "head", "augment")]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
-                    os.path.join(d, "libhonk_hip.so"), obj] + others, check=True)
+                    os.path.join(d, "libhonk_hip.so")] + objs + others, check=True)
     shutil.rmtree(src)
     for t in glob.glob(os.path.join(d, "*")):
         if not t.endswith((".so", "-gfx950.s")):

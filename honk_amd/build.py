@@ -10,7 +10,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhonk_hip.so")
-SOURCES = ["runtime.cpp", "res.hip", "cnn.hip", "train.hip", "mfcc.hip", "head.hip", "augment.hip"]
+SOURCES = ["runtime.cpp", "res.hip", "res_f16.hip", "cnn.hip", "train.hip", "mfcc.hip", "head.hip", "augment.hip"]
+# per-source extra flags / dependencies: res_f16.hip (the f16x2 pair and last-layer kernels)
+# includes res.hip and takes the MFMA accumulators in VGPRs (see its header)
+FLAGS = {"res_f16.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+DEPS = {"res_f16.hip": ["res.hip"]}
 ARCH = os.environ.get("HONK_OFFLOAD_ARCH", "gfx950")
 
 
@@ -71,9 +75,10 @@ def build(force=False, verbose=False):
         # incremental: an object newer than its source and every shared header is kept
         asm = os.path.join(tmp, src.rsplit(".", 1)[0] + "-hip-amdgcn-amd-amdhsa-gfx950.s")
         if not force and os.path.exists(obj) and (os.path.exists(asm) or not src.endswith(".hip")) and all(
-                os.path.getmtime(obj) > os.path.getmtime(p) for p in [os.path.join(CSRC, src)] + headers):
+                os.path.getmtime(obj) > os.path.getmtime(p)
+                for p in [os.path.join(CSRC, f) for f in [src] + DEPS.get(src, [])] + headers):
             continue
-        cmd = base + (["-x", "hip"] if src.endswith(".cpp") else []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = base + FLAGS.get(src, []) + (["-x", "hip"] if src.endswith(".cpp") else []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
