@@ -257,9 +257,9 @@ def build(name, patches=None):
     from honk_amd.build import FLAGS
     cc = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-function",
           "-save-temps=obj", "-I", os.path.join(src, "include")]
-    objs = []  # res.hip and res_f16.hip (the f16x2 pair / last layer, with their own flags)
+    objs = []  # res.hip and res_vf.hip (the f16x2 pair / last layer, with their own flags)
     procs = []
-    for tu in ("res.hip", "res_f16.hip"):
+    for tu in ("res.hip", "res_vf.hip"):
         objs.append(os.path.join(d, tu.replace(".hip", ".o")))
         procs.append(subprocess.Popen(cc + FLAGS.get(tu, []) + cflags + ["-c", os.path.join(csrc, tu), "-o", objs[-1]]))
     assert all(p.wait() == 0 for p in procs), name
@@ -280,7 +280,7 @@ sys.path.insert(0, os.getcwd())
 from honk_amd import model as hm
 torch.manual_seed(0)
 m = hm.find_model("res15")(dict(hm.find_config("res15"))).eval().cuda()
-m.honk_precision, m.honk_reroute = "f16x2", False
+m.honk_precision, m.honk_reroute = os.environ.get("PAIR_PREC", "f16x2"), False
 x = torch.randn(8192, 101, 40, device="cuda")
 with torch.no_grad():
     for _ in range(3):

@@ -10,11 +10,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhonk_hip.so")
-SOURCES = ["runtime.cpp", "res.hip", "res_f16.hip", "cnn.hip", "train.hip", "mfcc.hip", "head.hip", "augment.hip"]
-# per-source extra flags / dependencies: res_f16.hip (the f16x2 pair and last-layer kernels)
+SOURCES = ["runtime.cpp", "res.hip", "res_vf.hip", "cnn.hip", "train.hip", "mfcc.hip", "head.hip", "augment.hip"]
+# per-source extra flags / dependencies: res_vf.hip (the f16x2 pair and last-layer kernels)
 # includes res.hip and takes the MFMA accumulators in VGPRs (see its header)
-FLAGS = {"res_f16.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
-DEPS = {"res_f16.hip": ["res.hip"]}
+FLAGS = {"res_vf.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+DEPS = {"res_vf.hip": ["res.hip"]}
 ARCH = os.environ.get("HONK_OFFLOAD_ARCH", "gfx950")
 
 

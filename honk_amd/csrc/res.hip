@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256) void conv0_generic_kernel(const float* __restr
   }
 }
 
-#ifndef HONK_RES_F16_TU  // res_f16.hip: templates only (see there)
+#ifndef HONK_RES_VF_TU  // res_vf.hip: templates only (see there)
 // --------------------------------------------------------------------------- //
 // tail: logits[b] = Wout . mean_hw(x[b]) + bout      (x already BN-applied)
 // --------------------------------------------------------------------------- //
@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) void tail_sum_kernel(const float* __restrict__
   }
 }
 
-#endif  // HONK_RES_F16_TU
+#endif  // HONK_RES_VF_TU
 
 #include "res_bf16.inc"
 #include "res_bf16r.inc"
@@ -733,7 +733,7 @@ __global__ __launch_bounds__(256, 7) void conv0m_kernel(const float* __restrict_
   }
 }
 
-#ifndef HONK_RES_F16_TU
+#ifndef HONK_RES_VF_TU
 // --------------------------------------------------------------------------- //
 // weight packing
 // --------------------------------------------------------------------------- //
@@ -1506,9 +1506,10 @@ static int launch_block16n(const Layout& L, const __bf16* in, const float* frb, 
 // bf16 schedule: activations stay pre-BN (see res_bf16.inc), so one residual
 // stream R (conv0 output, then every even layer's sum, in place) and one odd-layer
 // buffer X suffice; each layer writes exactly one tensor.
-// res_f16.hip (compiled with its own flags): the f16x2 pair and last-layer launches
-bool launch_pair_f16(bool imm, int ppr, int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
-void launch_last_f16(int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
+// res_vf.hip (compiled with its own flags): the pair and last-layer launches
+bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd, hipStream_t st,
+                    const Block16PArgs& pa);
+void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 
 static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* packed, const float* x,
                         float* logits, int64_t batch, int64_t chunk, void* workspace, hipStream_t st) {
@@ -1595,16 +1596,10 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.padb = pp.padb;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(256 * pp.ns);
-            if (FM == 1 && pp.ppr == 9) hipLaunchKernelGGL((block16p_kernel<3, 2, 9, 9, 1>), gd, bd, 0, st, pa);
-            else if (FM == 1 && pp.ppr == 5) hipLaunchKernelGGL((block16p_kernel<3, 2, 5, 10, 1>), gd, bd, 0, st, pa);
-            else if (FM == 1) hipLaunchKernelGGL((block16p_kernel<3, 2, 3, 9, 1>), gd, bd, 0, st, pa);
-            else if (FM == 2) {
-              if (!launch_pair_f16(pp.ppr == 4 && pp.padb > 0, pp.ppr, dA, dil_of(d, i + 1), gd, bd, st, pa))
-                return fail(HONK_ERR_UNSUPPORTED, "block16p: no tap-step instance for dilations %d, %d", dA,
-                            dil_of(d, i + 1));
-            } else if (pp.ppr == 4 && pp.ns == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
-            else if (pp.ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1>), gd, bd, 0, st, pa);
-            else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 1>), gd, bd, 0, st, pa);
+            if (FM == 0 && pp.ns == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
+            else if (!launch_pair_vf(FM, pp.ppr, pp.ppr == 4 && pp.padb > 0, dA, dil_of(d, i + 1), gd, bd, st, pa))
+              return fail(HONK_ERR_UNSUPPORTED, "block16p: no tap-step instance for dilations %d, %d", dA,
+                          dil_of(d, i + 1));
             HONK_LAUNCH_CHECK("res block16p_kernel");
             tl.done(st);
             ++i;  // layer i + 1 done too
@@ -1632,9 +1627,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.chsum = chsum;
             TimedLaunch tl(st, layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(128 * lp.ns);
-            if (FM == 1) hipLaunchKernelGGL((block16l_kernel<3, 2, 9, 9, 2>), gd, bd, 0, st, pa);
-            else if (FM == 2) launch_last_f16(pa.d, gd, bd, st, pa);
-            else hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
+            launch_last_vf(FM, pa.d, gd, bd, st, pa);
             HONK_LAUNCH_CHECK("res block16l_kernel");
             tl.done(st);
             parts_last = 2;
@@ -1719,10 +1712,10 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
   }
 }
 
-#endif  // HONK_RES_F16_TU
+#endif  // HONK_RES_VF_TU
 }  // namespace res
 }  // namespace honk
-#ifndef HONK_RES_F16_TU
+#ifndef HONK_RES_VF_TU
 
 using namespace honk;
 using namespace honk::res;
@@ -2021,4 +2014,4 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
 }
 
 }  // extern "C"
-#endif  // HONK_RES_F16_TU
+#endif  // HONK_RES_VF_TU
