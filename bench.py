@@ -601,6 +601,7 @@ def measure_train(ctx, args, name="res26-narrow", B=None):
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     ctx.barrier()
+    reducer.remove()  # no gradient hooks outlive the timed steps
     per = hd.gather_scalar(t1 - t0, device=ctx.dev)
     el = max(per)
     fl = train_flops_per_clip(cfg)
