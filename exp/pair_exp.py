@@ -147,6 +147,7 @@ STAMP = [
     ("res.hip", "extern \"C\" {", "extern \"C\" {\n"
      "int honk_dbg_read(unsigned long long* h, int n) { (void)hipDeviceSynchronize(); return (int)hipMemcpy(h, honk::res::honk_dbg_buf(), n * 8, hipMemcpyDeviceToHost); }"),
 ]
+VARIANTS_OLD3 = []
 VARIANTS = {
     "stamp": STAMP,
     "stampsametq": STAMP + [("        if constexpr (S == KG) nxt = geo_t(wk);",
@@ -222,6 +223,24 @@ VARIANTS = {
     "nogeo2": [WALK2, GEO2],
     "nocok": [NOCOK],
     "novalid": [NOCOK, NOROK],
+    "oldsel": [("        return (tq[tB] & hi2) | (tq[tA] & ~hi2);",
+                "        if constexpr (TBL) return (tq[tB] & hi2) | (tq[tA] & ~hi2);\n        else return tq[tA] + ((tq[tB] - tq[tA]) & hi2);")],
+    "oldsel26": [("        return (tq[tB] & hi2) | (tq[tA] & ~hi2);",
+                "        if constexpr (TBL) return (tq[tB] & hi2) | (tq[tA] & ~hi2);\n        else return tq[tA] + ((tq[tB] - tq[tA]) & hi2);"),
+                 ("(NS * WPS > 4 ? 33 : 64)", "(NS * WPS > 4 ? 26 : 64)")],
+    "oldrelu": [("common.h", "{ return __builtin_elementwise_maximum(x, 0.f); }", "{ return x <= 0.f ? 0.f : x; }")],
+    "oldact": [("res_bf16w.inc", """          float r = act_dec<FM>(rv[f][0][e >> 1], e);
+          if constexpr (SP == 2) r += act_dec<FM>(rv[f][1][e >> 1], e);""", """          float r = 0.f;
+#pragma unroll
+          for (int pt = 0; pt < SP; ++pt) r += act_dec<FM>(rv[f][pt][e >> 1], e);""")],
+    "old3": VARIANTS_OLD3,
+    "pin24": [("(NS * WPS > 4 ? 33 : 64)", "(NS * WPS > 4 ? 24 : 64)")],
+    "pin28": [("(NS * WPS > 4 ? 33 : 64)", "(NS * WPS > 4 ? 28 : 64)")],
+    "pin26": [("(NS * WPS > 4 ? 33 : 64)", "(NS * WPS > 4 ? 26 : 64)")],
+    "pin30": [("(NS * WPS > 4 ? 33 : 64)", "(NS * WPS > 4 ? 30 : 64)")],
+    "pin36": [("(NS * WPS > 4 ? 33 : 64)", "(NS * WPS > 4 ? 36 : 64)")],
+    "pin40": [("(NS * WPS > 4 ? 33 : 64)", "(NS * WPS > 4 ? 40 : 64)")],
+    "pin20": [("(NS * WPS > 4 ? 33 : 64)", "(NS * WPS > 4 ? 20 : 64)")],
     "kg6": kwkg(3, 6),
     "kg3": kwkg(1, 3),
     "kg8": kwkg(4, 8),
@@ -229,6 +248,8 @@ VARIANTS = {
 
 
 def build(name, patches=None):
+    if name == "old3":
+        patches = VARIANTS["oldrelu"] + VARIANTS["oldact"] + VARIANTS["oldsel"]
     d = os.path.join(OUT, name)
     src = os.path.join(d, "src")
     shutil.rmtree(d, ignore_errors=True)
