@@ -396,6 +396,46 @@ def bench_model(name, dev):
     return model.eval().to(dev)
 
 
+def admission_report(dev):
+    """What ``auto`` does on the reference-written range fixtures (outside the timed
+    region): the realistic-scale res15-speech case (speech-like PCM -> MFCC, c0 about
+    -20..-150, BN calibrated on it) and an out-of-distribution batch (range_res15-ood:
+    inputs x 3000) fed to its unit-calibrated model after a calibrated batch -- the mode
+    picked, the clips the per-clip f16x2 admission re-ran in bf16x3, and the error against
+    the reference's logits (tests/golden/make_range_golden.py)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    try:
+        from golden_util import load_fixture, load_range_fixture
+    finally:
+        sys.path.pop(0)
+    from honk_amd import model as hm
+    out = {}
+
+    def one(m, x, want):
+        with torch.no_grad():
+            got = m(torch.as_tensor(x).to(dev)).cpu().numpy()
+        err = np.abs(got - want)
+        return {"mode": m.honk_last_precision, "rerun_clips": m.honk_last_rerun, "clips": len(x),
+                "max_abs_err": float(err.max()),
+                "max_err_over_bar": float((err / (1e-4 * np.maximum(1, np.abs(want).max(1, keepdims=True)))).max())}
+
+    def module(cfg, params, name):
+        m = hm.find_model(name)(cfg)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+        return m.eval().to(dev)
+
+    cfg, params, x, logits, name = load_range_fixture("res15-speech")
+    out["res15_speech_realistic"] = one(module(cfg, params, name), x, logits)
+    cfg, params, x, logits, meta = load_fixture("res15-b3-mfcc")
+    m = module(cfg, params, "res15")
+    out["res15_calibrated_then_ood"] = [one(m, x, logits)]
+    _, _, x, logits, _ = load_range_fixture("res15-ood")
+    out["res15_calibrated_then_ood"].append(one(m, x, logits))
+    out["note"] = ("auto = the reference callers' default; max_err_over_bar = |err| / (1e-4 max(1, |logit|)) "
+                   "per clip; the ood batch's clips leave the model's calibration (|z| > 8) and re-run in bf16x3")
+    return out
+
+
 def _plan_str(plan):
     return " + ".join(f"{k} x{plan.count(k)}" for k in sorted(set(plan), key=plan.index))
 
@@ -703,6 +743,7 @@ def rank_main(args):
         el, per, out, (kms, nlaunch, kflop) = ctx.timed(model, x, args.steps, args.warmup)
         parity = _sample_parity(model, cfg, x, out, orc, B)
     prec = model.honk_last_precision   # the mode the request resolved to (the policy's choice)
+    rerun = getattr(model, "honk_last_rerun", 0) if is_res else 0
 
     alts = {}
     if not args.no_alt and not args.e2e:
@@ -772,6 +813,16 @@ def rank_main(args):
             "roofline": roof,
             "parity": parity,
         }
+        if is_res:
+            res["f16x2_admission"] = {"rerun_clips_last_step": rerun, "z_max": 8,
+                                      "what": "every f16x2 batch is admitted per clip (tail_sum_kernel's flag, "
+                                              "flag_compact_kernel, one host sync per call); flagged clips "
+                                              "re-run in bf16x3 -- inside the timed steps"}
+            if args.model == "res15" and not args.e2e:
+                try:
+                    res["f16x2_admission"]["fixtures"] = admission_report(dev)
+                except Exception as e:  # a report, not the measurement
+                    res["f16x2_admission"]["fixtures"] = {"error": repr(e)}
         res.update(alts)
         if cpu is not None:
             res["cpu_baseline"] = cpu

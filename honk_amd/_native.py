@@ -53,6 +53,7 @@ _PROTOS = {
                                                  ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]),
     "honk_res_forward": (ctypes.c_int, [ctypes.POINTER(ResDesc), c_f32p, c_f32p, c_f32p, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_res_rerun_count": (ctypes.c_int64, []),
     "honk_cnn_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(CnnDesc), ctypes.c_int64]),
     "honk_cnn_forward": (ctypes.c_int, [ctypes.POINTER(CnnDesc), ctypes.POINTER(ctypes.c_void_p), c_f32p, c_f32p,
                                         ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),

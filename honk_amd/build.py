@@ -18,6 +18,11 @@ DEPS = {"res_vf.hip": ["res.hip"]}
 ARCH = os.environ.get("HONK_OFFLOAD_ARCH", "gfx950")
 
 
+def asm_path(build_dir, src):
+    """The device assembly -save-temps=obj keeps for one source (the spill guard's input)."""
+    return os.path.join(build_dir, src.rsplit(".", 1)[0] + f"-hip-amdgcn-amd-amdhsa-{ARCH}.s")
+
+
 def hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if c and os.path.exists(c):
@@ -30,8 +35,7 @@ def needs_build():
         return True
     tmp = os.path.join(HERE, "_build")
     for src in SOURCES:  # the device assembly the spill guard reads
-        if src.endswith(".hip") and not os.path.exists(
-                os.path.join(tmp, src.rsplit(".", 1)[0] + "-hip-amdgcn-amd-amdhsa-gfx950.s")):
+        if src.endswith(".hip") and not os.path.exists(asm_path(tmp, src)):
             return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
@@ -48,8 +52,12 @@ def check_spills(build_dir):
         import check_spills as cs
     finally:
         sys.path.pop(0)
-    paths = [os.path.join(build_dir, f) for f in sorted(os.listdir(build_dir))
-             if f.endswith("-hip-amdgcn-amd-amdhsa-gfx950.s")]
+    # exactly the current sources' assembly (not stale files of removed sources); every
+    # .hip source must have produced one, or the guard would silently scan nothing
+    paths = [asm_path(build_dir, src) for src in SOURCES if src.endswith(".hip")]
+    missing = [p for p in paths if not os.path.exists(p)]
+    if missing:
+        raise RuntimeError("spill guard: no device assembly for " + ", ".join(map(os.path.basename, missing)))
     bad = cs.check_files(paths, verbose=False)
     if bad:
         raise RuntimeError("split register spills (tools/check_spills.py):\n" +
@@ -73,7 +81,7 @@ def build(force=False, verbose=False):
         obj = os.path.join(tmp, src.rsplit(".", 1)[0] + ".o")
         objs.append(obj)
         # incremental: an object newer than its source and every shared header is kept
-        asm = os.path.join(tmp, src.rsplit(".", 1)[0] + "-hip-amdgcn-amd-amdhsa-gfx950.s")
+        asm = asm_path(tmp, src)
         if not force and os.path.exists(obj) and (os.path.exists(asm) or not src.endswith(".hip")) and all(
                 os.path.getmtime(obj) > os.path.getmtime(p)
                 for p in [os.path.join(CSRC, f) for f in [src] + DEPS.get(src, [])] + headers):

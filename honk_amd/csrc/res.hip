@@ -511,15 +511,18 @@ __global__ __launch_bounds__(256) void tail_sum_kernel(const float* __restrict__
                                                        const float* __restrict__ bn_scale,
                                                        const float* __restrict__ bn_shift,
                                                        const float* __restrict__ cscale,
-                                                       const float* __restrict__ oscale) {
+                                                       const float* __restrict__ oscale,
+                                                       int* __restrict__ flags, float zmax) {
   // groups of 64 threads sum every ng-th partial (coalesced rows of CP floats), then one
   // thread per channel adds the groups' sums in group order: a fixed order for every clip
   // (the row-band last layer writes 8 waves x MT m-tiles x bands partials per clip; one
   // thread walking all of them serially took 15 us per 4096-clip chunk)
   __shared__ float part[4][64];
   __shared__ float mean[64];
+  __shared__ int out_of_range;
   const int b = blockIdx.x;
   const int t = threadIdx.x, c = t & 63, grp = t >> 6, ng = blockDim.x >> 6;
+  if (t == 0) out_of_range = 0;
   float s = 0.f;
   if (c < CP) {
     const float* p = chsum + (size_t)b * nparts * CP + c;
@@ -533,8 +536,15 @@ __global__ __launch_bounds__(256) void tail_sum_kernel(const float* __restrict__
     // the f16x2 clip scale times the last layer's output exponent (powers of two: exact)
     if (cscale) v /= cscale[b] * *oscale;
     mean[t] = bn_scale ? fmaf(v / (float)HW, bn_scale[t], bn_shift[t]) : v / (float)HW;
+    // f16x2 admission (flags != null): the clip's BatchNorm'd last-layer channel means are
+    // its distance from the model's calibration, in standard deviations; beyond zmax (or
+    // not finite: an fp16 store overflowed) the clip is re-run in bf16x3 (honk_res_forward)
+    if (flags && t < C && !(fabsf(mean[t]) <= zmax)) out_of_range = 1;
   }
   __syncthreads();
+  // flags[b] == 2: the clip's input is not finite (clip_scale_kernel) -- its NaN logits are
+  // the reference's, nothing to re-run
+  if (flags && t == 0 && out_of_range && flags[b] != 2) flags[b] = 1;
   for (int n = t; n < NL; n += blockDim.x) {
     float acc = 0.f;
     for (int k = 0; k < C; ++k) acc = fmaf(wout[n * C + k], mean[k], acc);
@@ -926,8 +936,11 @@ __global__ __launch_bounds__(256) void pack_range_kernel(float* __restrict__ rec
 
 // The clip's power-of-two scale (see above): one wave per clip; a clip with a
 // non-finite input keeps s_model (its NaN / Inf propagates as in the reference).
+// flags (may be null): [n] the clips' admission flags, initialised here (2: the input is
+// not finite, else 0; tail_sum_kernel raises 1).
 __global__ __launch_bounds__(256) void clip_scale_kernel(const float* __restrict__ x, const float* __restrict__ rec,
-                                                         float* __restrict__ cscale, int n, int hw) {
+                                                         float* __restrict__ cscale, int n, int hw,
+                                                         int* __restrict__ flags) {
   const int lane = threadIdx.x & 63;
   const int clip = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (clip >= n) return;
@@ -964,7 +977,49 @@ __global__ __launch_bounds__(256) void clip_scale_kernel(const float* __restrict
     s = ldexpf(s, -ex);
   }
   s = fminf(fmaxf(s, 0x1p-24f), 0x1p14f);  // channel C holds s: an exact fp16 value
-  if (lane == 0) cscale[clip] = s;
+  if (lane == 0) {
+    cscale[clip] = s;
+    if (flags) flags[clip] = bad ? 2 : 0;
+  }
+}
+
+// The f16x2 admission's bookkeeping (honk_res_forward): the flagged clips' indices in
+// batch order (one workgroup, a fixed-order scan: the re-run is deterministic), then the
+// gather of their inputs and the scatter of their re-run logits.
+__global__ __launch_bounds__(1024) void flag_compact_kernel(const int* __restrict__ flags, int64_t n,
+                                                            int* __restrict__ list, int* __restrict__ count) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (n + 1023) / 1024, lo = t * per, hi = lo + per < n ? lo + per : n;
+  int k = 0;
+  for (int64_t i = lo; i < hi; ++i) k += flags[i] == 1;
+  part[t] = k;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan (Hillis-Steele)
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int w = part[t] - k;
+  for (int64_t i = lo; i < hi; ++i)
+    if (flags[i] == 1) list[w++] = (int)i;
+  if (t == 1023) *count = part[1023];
+}
+
+__global__ __launch_bounds__(256) void gather_clips_kernel(const float* __restrict__ x, const int* __restrict__ list,
+                                                           int hw, float* __restrict__ out) {
+  const float* src = x + (size_t)list[blockIdx.x] * hw;
+  float* dst = out + (size_t)blockIdx.x * hw;
+  for (int i = threadIdx.x; i < hw; i += blockDim.x) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(64) void scatter_logits_kernel(const float* __restrict__ src,
+                                                            const int* __restrict__ list, int n, int NL,
+                                                            float* __restrict__ logits) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n * NL) return;
+  logits[(size_t)list[i / NL] * NL + i % NL] = src[i];
 }
 
 // --------------------------------------------------------------------------- //
@@ -1511,8 +1566,11 @@ bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd,
                     const Block16PArgs& pa);
 void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 
+// flags (f16x2 only, may be null): [batch] the clips' admission flags (clip_scale_kernel,
+// tail_sum_kernel; honk_res_forward re-runs the flagged clips)
 static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* packed, const float* x,
-                        float* logits, int64_t batch, int64_t chunk, void* workspace, hipStream_t st) {
+                        float* logits, int64_t batch, int64_t chunk, void* workspace, hipStream_t st,
+                        int* flags = nullptr) {
   const int FM = fmt_of(L.prec);  // operand format (res_bf16w.inc)
   const int SP = sp_of(FM);       // 16-bit elements per channel value
   const size_t act = (size_t)chunk * L.H * L.W * L.CP * SP;
@@ -1542,7 +1600,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, 4, L.H * L.W, L.C, L.CP, L.NL, bn_last,
-                         bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
+                         bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE, (int*)nullptr, 0.f);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (whole stack)");
     }
     return HONK_OK;
@@ -1559,7 +1617,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       const int64_t n = (batch - c0 < chunk) ? batch - c0 : chunk;
       if (FM == 2) {
         hipLaunchKernelGGL(clip_scale_kernel, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, st, x + c0 * L.Hin * L.Win,
-                           packed + L.off_range, cscale, (int)n, L.Hin * L.Win);
+                           packed + L.off_range, cscale, (int)n, L.Hin * L.Win, flags ? flags + c0 : nullptr);
         HONK_LAUNCH_CHECK("res clip_scale_kernel");
       }
       rc = (FM == 1) ? launch_conv0_16<1, true>(L, x + c0 * L.Hin * L.Win, R, packed + L.off_conv0, n, st)
@@ -1662,7 +1720,8 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, parts_last, L.H * L.W, L.C, L.CP, L.NL,
-                         bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
+                         bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE,
+                         flags ? flags + c0 : nullptr, (float)HONK_F16X2_Z_MAX);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (weight-stationary)");
     }
     return HONK_OK;
@@ -1705,7 +1764,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, nbc_last * 8 * pr.MT, L.H * L.W, L.C, L.CP, L.NL,
-                         bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE);
+                         bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE, (int*)nullptr, 0.f);
       HONK_LAUNCH_CHECK("res tail_sum_kernel (bf16 row-band)");
     }
     return HONK_OK;
@@ -1769,7 +1828,10 @@ int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, i
   return cnt;
 }
 
-size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
+}  // extern "C"
+
+// honk_res_workspace_bytes without the f16x2 admission's regions (below)
+static size_t ws_bytes_plain(const honk_res_desc* d, int64_t batch) {
   Layout L;
   if (make_layout(d, &L) != HONK_OK || batch < 1) return 0;
   const int64_t ch = chunk_clips(L, batch);
@@ -1809,6 +1871,63 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
   const Plan p = plan_block(L);
   return (size_t)3 * ch * L.H * L.W * L.CP * sizeof(float) + (size_t)ch * p.nbands * MW * L.CP * sizeof(float);
 }
+
+// The f16x2 admission (HONK_PREC_F16X2, unless HONK_F16X2_RERUN=0): after the f16x2
+// pass, the clips tail_sum_kernel flagged are re-run in bf16x3, RC at a time, in the
+// f16x2 pass's (then free) activation region.  Workspace: [main | flags[batch] |
+// list[batch] | count | gathered inputs [RC] | re-run logits [RC]].
+struct F16Check {
+  int64_t rc;
+  size_t main, flags, list, count, gx, glog, total;
+};
+static bool f16x2_rerun_on() {
+  const char* e = getenv("HONK_F16X2_RERUN");
+  return !(e && e[0] == '0');
+}
+static honk_res_desc rerun_desc(const honk_res_desc* d) {
+  honk_res_desc e = *d;
+  e.precision = HONK_PREC_BF16X3;
+  return e;
+}
+static bool f16_check_plan(const honk_res_desc* d, int64_t batch, F16Check* p) {
+  Layout L;
+  if (make_layout(d, &L) != HONK_OK || batch < 1) return false;
+  const size_t f16 = ws_bytes_plain(d, batch);
+  const honk_res_desc e = rerun_desc(d);
+  if (f16 == 0) return false;
+  int64_t rc = chunk_clips(L, batch) / 2;
+  if (rc < 1) rc = 1;
+  while (rc > 1 && ws_bytes_plain(&e, rc) > f16) rc /= 2;
+  const size_t r = ws_bytes_plain(&e, rc);
+  if (r == 0) {
+    fail(HONK_ERR_UNSUPPORTED, "f16x2 admission: the bf16x3 re-run does not take this shape");
+    return false;
+  }
+  auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  p->rc = rc;
+  p->main = up(f16 > r ? f16 : r);
+  p->flags = p->main;
+  p->list = p->flags + up((size_t)batch * sizeof(int));
+  p->count = p->list + up((size_t)batch * sizeof(int));
+  p->gx = p->count + 256;
+  p->glog = p->gx + up((size_t)rc * L.Hin * L.Win * sizeof(float));
+  p->total = p->glog + up((size_t)rc * L.NL * sizeof(float));
+  return true;
+}
+
+static thread_local int64_t g_rerun = 0;
+
+extern "C" {
+
+size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch) {
+  if (d && d->precision == HONK_PREC_F16X2 && f16x2_rerun_on()) {
+    F16Check p;
+    return f16_check_plan(d, batch, &p) ? p.total : 0;
+  }
+  return ws_bytes_plain(d, batch);
+}
+
+int64_t honk_res_rerun_count(void) { return g_rerun; }
 
 int honk_res_pack(const honk_res_desc* d, const float* const* t, int32_t n_tensors, float* packed,
                   void* stream) {
@@ -1961,6 +2080,42 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
     return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", ws_bytes, need);
   hipStream_t st = (hipStream_t)stream;
   const int64_t chunk = chunk_clips(L, batch);
+  g_rerun = 0;
+  if (L.prec == HONK_PREC_F16X2 && f16x2_rerun_on()) {
+    if (batch > 0x7fffffff) return fail(HONK_ERR_ARG, "f16x2: batch beyond 2^31 clips");
+    F16Check p;
+    if (!f16_check_plan(d, batch, &p)) return fail(HONK_ERR_UNSUPPORTED, "%s", get_error());
+    char* ws = (char*)workspace;
+    int* flags = (int*)(ws + p.flags);
+    int* list = (int*)(ws + p.list);
+    int* count = (int*)(ws + p.count);
+    rc = forward_bf16(L, d, packed, x, logits, batch, chunk, workspace, st, flags);
+    if (rc) return rc;
+    hipLaunchKernelGGL(flag_compact_kernel, dim3(1), dim3(1024), 0, st, flags, batch, list, count);
+    HONK_LAUNCH_CHECK("res flag_compact_kernel");
+    int flagged = 0;
+    HONK_HIP_CHECK(hipMemcpyAsync(&flagged, count, sizeof(int), hipMemcpyDeviceToHost, st));
+    HONK_HIP_CHECK(hipStreamSynchronize(st));
+    g_rerun = flagged;
+    if (flagged == 0) return HONK_OK;
+    const honk_res_desc e = rerun_desc(d);
+    Layout L3;
+    rc = make_layout(&e, &L3);
+    if (rc) return rc;
+    float* gx = (float*)(ws + p.gx);
+    float* glog = (float*)(ws + p.glog);
+    for (int64_t o = 0; o < flagged; o += p.rc) {
+      const int64_t n = flagged - o < p.rc ? flagged - o : p.rc;
+      hipLaunchKernelGGL(gather_clips_kernel, dim3((unsigned)n), dim3(256), 0, st, x, list + o, L.Hin * L.Win, gx);
+      HONK_LAUNCH_CHECK("res gather_clips_kernel");
+      rc = forward_bf16(L3, &e, packed, gx, glog, n, chunk_clips(L3, n), workspace, st);
+      if (rc) return rc;
+      hipLaunchKernelGGL(scatter_logits_kernel, dim3((unsigned)cdiv(n * L.NL, 64)), dim3(64), 0, st, glog, list + o,
+                         (int)n, L.NL, logits);
+      HONK_LAUNCH_CHECK("res scatter_logits_kernel");
+    }
+    return HONK_OK;
+  }
   if (L.prec != HONK_PREC_F32) return forward_bf16(L, d, packed, x, logits, batch, chunk, workspace, st);
   const size_t act = (size_t)chunk * L.H * L.W * L.CP;
   float* R = (float*)workspace;
@@ -2006,7 +2161,7 @@ int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, p.nbands * MW, L.H * L.W, L.C, L.CP, L.NL,
                          (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
-                         (const float*)nullptr);
+                         (const float*)nullptr, (int*)nullptr, 0.f);
       HONK_LAUNCH_CHECK("res tail_sum_kernel");
     }
   }

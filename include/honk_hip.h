@@ -154,9 +154,24 @@ int honk_res_numerics(const honk_res_desc* d, const float* packed, float* rec, i
  */
 int honk_res_select_precision(const honk_res_desc* d, const float* rec, int32_t requested, char* note,
                               size_t note_len);
-/* x: [batch, height, width] fp32;  logits: [batch, n_labels] fp32 (eval-mode forward) */
+/*
+ * x: [batch, height, width] fp32;  logits: [batch, n_labels] fp32 (eval-mode forward)
+ *
+ * HONK_PREC_F16X2 admits every clip on its own (per batch, not once per model): after the
+ * f16x2 pass, a clip whose last-layer BatchNorm'd channel means lie beyond
+ * HONK_F16X2_Z_MAX standard deviations of the model's calibration (an input far outside
+ * the distribution the running statistics describe: f16x2's rounding is no longer
+ * averaged away there), or whose f16x2 logits are not finite while its input is, is
+ * re-run in BF16X3 and its logits replaced.  This is the one honk_res_forward mode that
+ * SYNCHRONISES `stream` (once per call, to read the flagged-clip count; not capturable
+ * in a hipGraph).  HONK_F16X2_RERUN=0 in the environment turns the admission off (raw
+ * f16x2: kernel tests).  The workspace (honk_res_workspace_bytes) includes its buffers.
+ */
 int honk_res_forward(const honk_res_desc* d, const float* packed, const float* x, float* logits,
                      int64_t batch, void* workspace, size_t workspace_bytes, void* stream);
+#define HONK_F16X2_Z_MAX 8
+/* The clips the calling thread's last honk_res_forward re-ran in bf16x3 (0 unless F16X2). */
+int64_t honk_res_rerun_count(void);
 
 /* ---- SpeechModel (cnn-*); utils/model.py:123-205 ------------------------------ */
 typedef struct honk_cnn_desc {

@@ -201,6 +201,30 @@ def test_abi_queries_without_gpu():
     assert b"gfx950" in lib.honk_version()
 
 
+def test_f16x2_admission_workspace(monkeypatch):
+    """f16x2's per-clip admission (honk_res_forward re-runs out-of-calibration clips in
+    bf16x3): its workspace = the f16x2 pass's (which the re-run reuses, half the chunk at
+    a time) + flags and index list per clip + the gathered inputs and re-run logits."""
+    _lib_path()
+    lib = _native.load()
+    d = _native.ResDesc(n_labels=12, n_maps=45, n_layers=13, use_dilation=1, pool_h=0, pool_w=0,
+                        height=101, width=40, precision=_native.PRECISIONS["f16x2"])
+    up = lambda v: (v + 255) // 256 * 256  # noqa: E731
+    for B in (1, 10, 4096, 10000):
+        monkeypatch.setenv("HONK_F16X2_RERUN", "0")
+        raw = lib.honk_res_workspace_bytes(d, B)
+        monkeypatch.delenv("HONK_F16X2_RERUN")
+        got = lib.honk_res_workspace_bytes(d, B)
+        rc = max(1, min(B, 4096) // 2)
+        d3 = _native.ResDesc(**{f: getattr(d, f) for f, _ in d._fields_})
+        d3.precision = _native.PRECISIONS["bf16x3"]
+        while rc > 1 and lib.honk_res_workspace_bytes(d3, rc) > raw:
+            rc //= 2
+        main = up(max(raw, lib.honk_res_workspace_bytes(d3, rc)))
+        assert raw > 0 and got == main + 2 * up(4 * B) + 256 + up(rc * 101 * 40 * 4) + up(rc * 12 * 4), B
+    assert lib.honk_res_rerun_count() == 0  # nothing ran on this thread
+
+
 def test_missing_extension_fails_loudly():
     saved = _native._lib
     _native._lib = None

@@ -106,6 +106,24 @@ def test_res_wide_models_run_on_layer_kernels():
         np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=ATOL, rtol=0)
 
 
+@pytest.mark.parametrize("maps", [65, 96])
+def test_res_wide_models_default_precision(maps):
+    """the DEFAULT precision ("auto", reroute on) on a model beyond every
+    packed kernel (more than 64 maps) -- the policy has no packed buffer to read; the
+    forward takes the layer-level fp32 kernels with the warning, at the fp32 bar."""
+    import warnings
+    cfg = dict(ref_configs()["res8"], n_feature_maps=maps)
+    params, x = _res_case(cfg, 3, seed=maps)
+    m = module(cfg, params, "res8")
+    assert m.honk_precision == "auto" and m.honk_reroute
+    with warnings.catch_warnings(record=True) as ws:
+        warnings.simplefilter("always")
+        out = run(m, x)
+    msgs = [str(w.message) for w in ws if issubclass(w.category, RuntimeWarning)]
+    assert any("layer-level fp32 kernels" in s for s in msgs), msgs
+    np.testing.assert_allclose(out, orc.forward(params, cfg, x), atol=ATOL, rtol=0)
+
+
 @pytest.mark.parametrize("name,B", [("cnn-trad-pool2", 3), ("cnn-one-fstride4", 5), ("cnn-tpool2", 2),
                                     ("cnn-tstride8", 4), ("cnn-one-stride1", 1)])
 def test_cnn_vs_oracle(name, B):

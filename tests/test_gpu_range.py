@@ -40,7 +40,7 @@ def _need_gpu():
 
 @pytest.fixture(autouse=True)
 def _no_env(monkeypatch):
-    for v in ("HONK_PRECISION", "HONK_RES_KERNEL", "HONK_LAST_KERNEL", "HONK_CONV0"):
+    for v in ("HONK_PRECISION", "HONK_RES_KERNEL", "HONK_LAST_KERNEL", "HONK_CONV0", "HONK_F16X2_RERUN"):
         monkeypatch.delenv(v, raising=False)
 
 
@@ -67,7 +67,7 @@ def run(m, x, expect_warning=None):
     return out.cpu().numpy()
 
 
-@pytest.mark.parametrize("name", ["res15-k2000", "res15-c0"])
+@pytest.mark.parametrize("name", ["res15-k2000", "res15-c0", "res15-speech"])
 def test_f16x2_range_fixtures_hold_1e4(name):
     """The f16x2 kernels themselves (no policy) on inputs whose pre-BN values leave
     fp16's range (k2000) or carry c0 at -1e3..-1e4: finite, within 1e-4."""
@@ -81,7 +81,7 @@ def test_f16x2_range_fixtures_hold_1e4(name):
     np.testing.assert_allclose(out, logits, atol=ATOL, rtol=0)
 
 
-@pytest.mark.parametrize("name", ["res15-k2000", "res15-c0"])
+@pytest.mark.parametrize("name", ["res15-k2000", "res15-c0", "res15-speech"])
 @pytest.mark.parametrize("prec", ["f16x2", "auto"])
 def test_policy_on_range_fixtures(name, prec):
     """auto / f16x2 with the policy: whichever mode the numerics record and the measured
@@ -96,10 +96,12 @@ def test_policy_on_range_fixtures(name, prec):
     np.testing.assert_allclose(out, logits, atol=ATOL, rtol=0)
 
 
-def test_f16x2_out_of_distribution_stays_finite():
+def test_f16x2_out_of_distribution_stays_finite(monkeypatch):
     """x 3000 on the unit-calibrated res15-b3-mfcc model: conv0's output passes 1.8e5;
     the clip scale keeps it in fp16's range.  The reference's logits reach ~2e3; f16x2's
-    relative error there is its rounding (2^-12 per stored value), as bf16x3's is its own."""
+    relative error there is its rounding (2^-12 per stored value), as bf16x3's is its own.
+    Raw f16x2 (the per-clip admission off: it would re-run these clips in bf16x3)."""
+    monkeypatch.setenv("HONK_F16X2_RERUN", "0")
     cfg, params, x, logits, model = load_range_fixture("res15-ood")
     out = {}
     for prec in ("f16x2", "bf16x3", "f32"):
@@ -115,7 +117,7 @@ def test_f16x2_out_of_distribution_stays_finite():
     assert (out["f16x2"].argmax(1) == logits.argmax(1)).all()
 
 
-@pytest.mark.parametrize("name", ["res15-k2000", "res15-ood", "res8-k2000"])
+@pytest.mark.parametrize("name", ["res15-k2000", "res15-ood", "res8-k2000", "res15-speech"])
 def test_numerics_record_matches_restatement(name):
     cfg, params, x, logits, model = load_range_fixture(name)
     m = module(cfg, params, model)
@@ -200,3 +202,60 @@ def test_unchanged_callers_run_the_fast_kernels(tmp_path, capsys, monkeypatch):
     seen.clear()
     tc.test_service_label_gpu_matches_reference_caller(tmp_path)
     assert seen and all(s[:2] == ("cnn", "bf16x3") for s in seen), seen
+
+
+def _rel_bound(logits):
+    """The probe's bar, per clip: half the 1e-4 bar, relative beyond |logit| = 1."""
+    return 5e-5 * np.maximum(1.0, np.abs(logits).max(axis=1, keepdims=True))
+
+
+def test_auto_admits_every_batch_clip_by_clip():
+    """f16x2 is admitted per clip, on every batch.  auto on the
+    unit-calibrated res15-b3-mfcc model takes f16x2 on its calibrated first batch (nothing
+    re-run); a later batch of the same model's inputs x 3000 (range_res15-ood, written by
+    the reference) runs under the same mode, and the per-clip admission re-runs each of
+    its clips in bf16x3 -- every logit within 5e-5 max(1, |logit|) of the reference's.
+    A mixed batch re-runs exactly the out-of-calibration clips; the others keep their
+    f16x2 logits bit for bit."""
+    cfg, params, x, logits, meta = load_fixture("res15-b3-mfcc")
+    m = module(cfg, params, "res15")
+    out1 = run(m, x)
+    assert m.honk_last_precision == "f16x2" and m.honk_last_rerun == 0
+    np.testing.assert_allclose(out1, logits, atol=ATOL, rtol=0)
+    _, p_ood, x_ood, l_ood, _ = load_range_fixture("res15-ood")
+    assert all(np.array_equal(params[k], p_ood[k]) for k in params)  # the same model
+    out2 = run(m, x_ood)
+    assert m.honk_last_precision == "f16x2" and m.honk_last_rerun == len(x_ood)
+    err = np.abs(out2 - l_ood)
+    print(f"ood batch under auto: max rel err {float((err / _rel_bound(l_ood)).max()) * 5e-5:.2e}")
+    assert (err <= _rel_bound(l_ood)).all()
+    xm = np.stack([x[0], x_ood[0], x[1], x_ood[1], x[2], x_ood[2]])
+    lm = np.stack([logits[0], l_ood[0], logits[1], l_ood[1], logits[2], l_ood[2]])
+    out3 = run(m, xm)
+    assert m.honk_last_rerun == 3
+    assert np.array_equal(out3[0::2], out1)  # the f16x2 clips: batch-position invariant
+    assert (np.abs(out3 - lm) <= _rel_bound(lm)).all()
+    # the re-run clips equal a bf16x3 forward of the same clips
+    m3 = module(cfg, params, "res15", "bf16x3")
+    np.testing.assert_allclose(out3[1::2], run(m3, x_ood), rtol=0, atol=1e-3)
+
+
+def test_admission_flags_only_out_of_calibration_clips():
+    """The admission's statistic on the bench's own workload: MFCC-like clips on a model
+    calibrated to them re-run nothing (the headline pays only the flag pass), scaled
+    inputs re-run once their last-layer channel means leave HONK_F16X2_Z_MAX (8) standard
+    deviations, and an input NaN is the reference's NaN, not a re-run."""
+    import bench
+    m = bench.bench_model("res15", torch.device(DEV))
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    x = bench.mfcc_like(256, DEV, g)
+    with torch.no_grad():
+        m(x)
+        assert m.honk_last_precision == "f16x2" and m.honk_last_rerun == 0
+        m(x * 64)
+        assert m.honk_last_rerun == 256
+        x[3, 5, 7] = float("nan")
+        out = m(x)
+        assert m.honk_last_rerun == 0
+        assert torch.isnan(out[3]).all() and torch.isfinite(out[torch.arange(256) != 3]).all()

@@ -8,10 +8,19 @@ its consumer reads it -- is only slow; a split one is the miscompile's shape.
 
 The check, per kernel of the device assembly (what ``honk_amd.build`` keeps from
 ``-save-temps``):
-  * every ``... Folded Reload`` into registers D: the first later instruction that reads
-    a register of D must read it through an operand that lies INSIDE D (the tuple the
-    spill saved, or a part of it).  An operand reaching past D -- e.g. a 16-byte MFMA
-    operand fed by a 12-byte reload -- was assembled from a partial restore: SPLIT;
+  * every ``... Folded Reload`` into registers D: EVERY later read of a register of D
+    while it still holds the reloaded value must go through an operand that lies INSIDE
+    D (the tuple the spill saved, or a part of it).  An operand reaching past D -- e.g. a
+    16-byte MFMA operand fed by a 12-byte reload -- was assembled from a partial restore:
+    SPLIT.  A register stops being followed once an instruction writes it; the scan runs
+    to the end of the kernel and, when the reload sits inside a loop (a backward branch
+    over it), around the back edge from the loop head to the reload, so a reload at the
+    bottom of a loop feeding the loop head is seen (paths are over-approximated:
+    conservative);
+  * any 8- or 12-byte ``Folded Spill`` of registers S (a part of a 16-byte MFMA operand
+    is the miscompile's shape) whose registers some instruction of the kernel reads
+    through an operand wider than S that overlaps it: SPLIT (a backstop; it can fire on
+    an unrelated later use of the same registers -- then review and WHITELIST);
   * any "Reload Reuse" annotation: SPLIT.
 Whole-tuple spills are listed for information.  A SPLIT fails the build (honk_amd.build)
 and the CPU test (tests/test_spills.py) unless the kernel is in WHITELIST with a reason.
@@ -50,42 +59,84 @@ def _demangle(name):
         return name
 
 
+_STORE = ("ds_write", "ds_store", "buffer_store", "global_store", "scratch_store", "flat_store")
+
+
+def _parse(line):
+    """(mnemonic, destination registers, source registers) of one instruction line."""
+    c = line.split(";", 1)[0].strip()
+    if not c or c.startswith(".") or c.endswith(":"):
+        return None
+    mnem, _, ops = c.partition(" ")
+    regs = _regs(ops)
+    if mnem.startswith(_STORE) or "store" in mnem:
+        return mnem, [], regs
+    return mnem, regs[:1], regs[1:]
+
+
+def _loops(lines):
+    """[(head, branch)] line ranges of backward branches (s_branch / s_cbranch_* to a
+    label above them)."""
+    labels, out = {}, []
+    for i, ln in enumerate(lines):
+        t = ln.split(";", 1)[0].strip()
+        if t.endswith(":"):
+            labels[t[:-1]] = i
+        elif t.startswith(("s_branch", "s_cbranch")):
+            tgt = t.split()[-1]
+            if tgt in labels:
+                out.append((labels[tgt], i))
+    return out
+
+
 def scan_kernel(body):
     """(status, detail) of one kernel body: status None (no spill), "spill" or "SPLIT"."""
-    lines = [ln.split(";", 1) for ln in body.split("\n")]
+    lines = body.split("\n")
+    parsed = [_parse(ln) for ln in lines]
     sizes, splits = [], []
     if "Reload Reuse" in body:
         splits.append("Reload Reuse annotation")
-    for i, parts in enumerate(lines):
-        if len(parts) < 2:
-            continue
-        code, note = parts
+    loops = _loops(lines)
+    for i, ln in enumerate(lines):
+        note = ln.split(";", 1)[1] if ";" in ln else ""
         if "Folded Spill" in note:
-            sizes.append(re.search(r"(\d+)-byte", note).group(1))
-        if "Folded Reload" not in note:
+            nb = int(re.search(r"(\d+)-byte", note).group(1))
+            sizes.append(str(nb))
+            src = parsed[i][2] if parsed[i] else []
+            if nb in (8, 12) and src:
+                f, a, b = src[0]
+                for j, pr in enumerate(parsed):
+                    wide = [r for r in (pr[1] + pr[2] if pr else []) if r[0] == f and
+                            not (r[2] < a or r[1] > b) and (r[1] < a or r[2] > b)]
+                    if wide:
+                        splits.append(f"{nb}-byte spill of {f}[{a}:{b}]; {f}[{wide[0][1]}:{wide[0][2]}] is read "
+                                      f"whole in `{lines[j].strip()[:80]}`")
+                        break
+        if "Folded Reload" not in note or not parsed[i] or not parsed[i][1]:
             continue
-        dst = _regs(code)
-        if not dst:
-            continue
-        f, a, b = dst[0]
-        for code2, *_ in lines[i + 1:]:
-            c = code2.strip()
-            if not c or c.startswith((".", "s_")):
+        f, a, b = parsed[i][1][0]
+        # successors: the rest of the kernel, then around each enclosing loop's back edge
+        order = list(range(i + 1, len(lines)))
+        for head, br in loops:
+            if head <= i <= br:
+                order += list(range(head, i))
+        live = set(range(a, b + 1))
+        for j in order:
+            pr = parsed[j]
+            if pr is None:
                 continue
-            mnem, _, ops = c.partition(" ")
-            regs = _regs(ops)
-            # the first register operand is the destination, except for stores / LDS writes
-            srcs = regs if ("store" in mnem or "write" in mnem) else regs[1:]
-            hit = [r for r in srcs if r[0] == f and not (r[2] < a or r[1] > b)]
-            if not hit:
-                if regs and srcs is not regs and regs[0][0] == f and not (regs[0][2] < a or regs[0][1] > b):
-                    break  # redefined before any read
-                continue
+            mnem, dst, srcs = pr
+            hit = [r for r in srcs if r[0] == f and any(r[1] <= k <= r[2] for k in live)]
             wide = [r for r in hit if r[1] < a or r[2] > b]
             if wide:
                 splits.append(f"{b - a + 1}-dword reload {f}[{a}:{b}] feeds {f}[{wide[0][1]}:{wide[0][2]}] "
-                              f"in `{c[:80]}`")
-            break
+                              f"in `{lines[j].strip()[:80]}`")
+                break
+            for r in dst:
+                if r[0] == f:
+                    live -= set(range(r[1], r[2] + 1))
+            if not live:
+                break
     if splits:
         return "SPLIT", "; ".join(splits)
     if sizes:
