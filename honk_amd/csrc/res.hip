@@ -1212,6 +1212,7 @@ struct PairPlan {
   int lag, NRA, NRB, slotb, ppr, ppw;  // ppw: DMA pieces per A wave per step
   int padb;                            // f16x2: zero-column bytes each side of a slot's row
   int ns;                              // streams per workgroup (block16p_kernel NS)
+  bool tbl;                            // bf16 two streams: the row-table instance (SCA = -1)
 };
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i);
 static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
@@ -1236,8 +1237,9 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
 // Fused pair plan (res_bf16p.inc) for layers A (dilation d) and B (tap stride sB
 // class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
-static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int nstreams = 1, bool padcols = false) {
-  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams};
+static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int nstreams = 1, bool padcols = false,
+                          bool tbl = false) {
+  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams, tbl};
   const int SP = sp_of(FM);
   const int P = 64, W = L.W, H = L.H;
   const long PXB = g16p_pxb(L.NT, SP);  // LDS pixel pitch
@@ -1310,7 +1312,8 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   if (F(-1) < 0) return pp;
   pp.NRA = (int)(nra > 2 ? nra : 2);
   pp.NRB = (int)(nrb > 2 ? nrb : 2);
-  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + g16p_lds_extra(FM, 4, pp.slotb) <= g16p_lds_bytes() / nstreams;
+  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + g16p_lds_extra(FM == 2 || padcols || tbl, 4, pp.slotb) <=
+          g16p_lds_bytes() / nstreams;
   return pp;
 }
 
@@ -1327,12 +1330,12 @@ static int pair_ppw(int SP, int ppr) {
 // f16x2 pairs with an instantiated compile-time tap step (block16p_kernel SCA / SCB: res15's
 // dilation pairs on 40-pixel rows): their rings carry pad columns (plan_pair padcols)
 static bool pair_imm(const Layout& L, int FM, int dA, int dB) {
-  if (FM != 2 || L.W != 40 || L.NT != 3) return false;
+  if ((FM != 2 && FM != 0) || L.W != 40 || L.NT != 3) return false;
   return (dA == 1 && (dB == 1 || dB == 2)) || (dA == 2 && dB == 2) || (dA == 4 && (dB == 4 || dB == 8)) ||
          (dA == 8 && dB == 8);
 }
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i) {
-  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1};
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1, false};
   const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
@@ -1343,8 +1346,13 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
   if (!sB || cb >= 0xE0000000ull) return no;
   // bf16 with full 40-pixel rows: two streams per workgroup when both rings fit half the LDS
   const char* nse = getenv("HONK_PAIR_STREAMS");
+  // (round 6: on the row-table walk, block16p_kernel<..., 2, 0, -1, -1>: its smaller per-wave
+  // state fits 256 registers with 32 weight fragments pinned and no spill -- res15 bf16 408K
+  // -> 469K clips/s against the walk-based two-stream kernel (19 spilled values reloaded in
+  // its step loop, now removed), 416K with one stream on the tap-step instances, same box;
+  // HONK_PAIR_STREAMS=1 selects those)
   if (FM == 0 && !(nse && nse[0] == '1')) {
-    const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2);
+    const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, false, true);
     if (p2.ok && p2.ppr == 4 && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
   }
   const PairPlan pp = plan_pair(L, FM, dA, sB, (int)cdiv(n, grid), 1, pair_imm(L, FM, dA, dB));
@@ -1359,7 +1367,7 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
 // (no A-out ring: NRB = 1 unused slot, no lag).  HONK_LAST_KERNEL=w keeps the
 // weight-stationary kernel (the pair-vs-w bitwise tests).
 static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) {
-  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1};
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1, false};
   const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   const char* lenv = getenv("HONK_LAST_KERNEL");
@@ -1373,7 +1381,7 @@ static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) 
   pp.NRB = 1;
   pp.lag = 0;
   pp.ns = ns;
-  pp.ok = (long)(pp.NRA + 1) * pp.slotb + g16p_lds_extra(FM, 2, pp.slotb) <= g16p_lds_bytes() / ns;
+  pp.ok = (long)(pp.NRA + 1) * pp.slotb + g16p_lds_extra(FM == 2, 2, pp.slotb) <= g16p_lds_bytes() / ns;
   return pp.ok ? pp : no;
 }
 
@@ -1565,6 +1573,7 @@ static int launch_block16n(const Layout& L, const __bf16* in, const float* frb, 
 bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd, hipStream_t st,
                     const Block16PArgs& pa);
 void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
+void launch_pair2t_vf(dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 
 // flags (f16x2 only, may be null): [batch] the clips' admission flags (clip_scale_kernel,
 // tail_sum_kernel; honk_res_forward re-runs the flagged clips)
@@ -1654,7 +1663,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.padb = pp.padb;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(256 * pp.ns);
-            if (FM == 0 && pp.ns == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
+            if (FM == 0 && pp.ns == 2) launch_pair2t_vf(gd, bd, st, pa);
             else if (!launch_pair_vf(FM, pp.ppr, pp.ppr == 4 && pp.padb > 0, dA, dil_of(d, i + 1), gd, bd, st, pa))
               return fail(HONK_ERR_UNSUPPORTED, "block16p: no tap-step instance for dilations %d, %d", dA,
                           dil_of(d, i + 1));

@@ -4,9 +4,9 @@
 // epilogue reads them directly instead of copying each m-tile's results out of AGPRs
 // first (f16x2: 12 v_accvgpr_read + 12 v_mov_b64 per step fewer, 1.87 -> 1.82 ms per
 // res15 pair launch, 1.00 -> 0.99 ms for the last layer, same box).
-// The flag is per compilation, and under it the two-stream bf16 pair kernel
-// (<3,1,4,4,2,0>) splits a spill reload, which the spill guard refuses -- so that one
-// and every other kernel stay in res.hip.
+// The flag is per compilation (the walk-based two-stream bf16 pair kernel split a spill
+// reload under it -- round 6 replaced that kernel by the row-table one below, which
+// does not spill); every other kernel stays in res.hip.
 //
 // This file includes res.hip with HONK_RES_VF_TU defined: the device templates and
 // their argument structs only (no host code, no non-template kernels), and defines
@@ -23,10 +23,11 @@ namespace res {
 // HONK_ERR_UNSUPPORTED); the two-stream bf16 instance (ns == 2) is not here.
 bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd, hipStream_t st,
                     const Block16PArgs& pa) {
-  if (FM == 2 && imm) {
+  if ((FM == 2 || FM == 0) && imm) {
 #define HONK_PI(a_, b_)                                                                              \
   if (dA == a_ && dB == b_) {                                                                        \
-    hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1, 2, a_, b_>), gd, bd, 0, st, pa);             \
+    if (FM == 2) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1, 2, a_, b_>), gd, bd, 0, st, pa); \
+    else hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1, 0, a_, b_>), gd, bd, 0, st, pa);        \
     return true;                                                                                     \
   }
     HONK_PI(1, 1) HONK_PI(1, 2) HONK_PI(2, 2) HONK_PI(4, 4) HONK_PI(4, 8) HONK_PI(8, 8)
@@ -41,6 +42,12 @@ bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd,
   else if (ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 1>), gd, bd, 0, st, pa);
   else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 1>), gd, bd, 0, st, pa);
   return true;
+}
+
+// bf16, two streams per workgroup on the row-table walk (SCA = -1: no tap-step
+// immediates -- the two streams' rings leave no room for pad columns)
+void launch_pair2t_vf(dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
+  hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2, 0, -1, -1>), gd, bd, 0, st, pa);
 }
 
 // the last (odd) layer with its channel sums (dilation d)

@@ -1,7 +1,9 @@
 """bf16 precision mode of the res path (configs C3/C4): bf16 activations and
-weights, fp32 accumulation.  Parity = top-1 agreement with the float64 oracle
-plus a logit error bound (SURVEY §7 'Parity vs precision'); bitwise batch
-invariance like the fp32 path."""
+weights, fp32 accumulation.  Parity (SURVEY §7 'Parity vs precision'): an a-priori
+logit error bound, and top-1 agreement with the reference on EVERY clip whose
+reference top-1 / top-2 logit gap exceeds twice that bound (a clip inside the bound
+of a tie is reported, not counted: no fp32 implementation decides those either);
+bitwise batch invariance like the fp32 path."""
 import numpy as np
 import pytest
 import torch
@@ -13,8 +15,25 @@ from golden_util import ref_configs
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-MAX_ABS = 0.05      # |logit - oracle| bound in bf16 (calibrated nets: logits O(0.5))
-MIN_TOP1 = 0.9      # top-1 agreement with the oracle
+# a-priori |logit - reference| bound of bf16 on BatchNorm-calibrated nets, relative beyond
+# |logit| = 1 (measured <= 3.4e-3 on every config)
+BF16_BOUND = 8e-3
+
+
+def margin_check(out, ref, what, bound=BF16_BOUND):
+    """err <= bound * max(1, |ref|); argmax agrees wherever the reference's top-1 / top-2
+    gap exceeds 2 x that bound.  Returns (max err, near-tie clips, flips among them)."""
+    b = bound * max(1.0, float(np.abs(ref).max()))
+    err = float(np.abs(out - ref).max())
+    top2 = np.sort(ref, axis=1)[:, -2:]
+    decided = (top2[:, 1] - top2[:, 0]) > 2 * b
+    agree = out.argmax(1) == ref.argmax(1)
+    near, flips = int((~decided).sum()), int((~agree).sum())
+    print(f"{what}: bf16 max|err| {err:.2e} (bound {b:.1e}); {len(ref)} clips, {near} within 2 x bound of a "
+          f"tie, {flips} top-1 flips (all among those)")
+    assert err <= b, (what, err, b)
+    assert agree[decided].all(), (what, np.nonzero(decided & ~agree))
+    return err, near, flips
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -51,11 +70,7 @@ def test_bf16_vs_oracle(name, B):
     cfg, params, x, m = _case(name, B, seed=7)
     out = _run(m, x)
     ref = orc.forward(params, cfg, x)
-    err = np.abs(out - ref).max()
-    top1 = np.mean(out.argmax(1) == ref.argmax(1))
-    print(f"{name}: bf16 max|err|={err:.3e} top1={top1:.3f}")
-    assert err <= MAX_ABS, err
-    assert top1 >= MIN_TOP1, top1
+    margin_check(out, ref, name)
 
 
 @pytest.mark.parametrize("override", [dict(n_feature_maps=16), dict(n_feature_maps=32), dict(n_layers=1),
@@ -64,8 +79,7 @@ def test_bf16_overrides(override):
     cfg, params, x, m = _case("res8", 32, seed=3, override=override)
     out = _run(m, x)
     ref = orc.forward(params, cfg, x)
-    assert np.abs(out - ref).max() <= MAX_ABS
-    assert np.mean(out.argmax(1) == ref.argmax(1)) >= MIN_TOP1
+    margin_check(out, ref, f"res8 {override}")
 
 
 def test_bf16_mfcc_like_inputs():
@@ -81,11 +95,30 @@ def test_bf16_mfcc_like_inputs():
     m = m.to(DEV)
     out = _run(m, x)
     ref = orc.forward(params, cfg, x)
-    scale_ref = np.abs(ref).max()
-    err = np.abs(out - ref).max()
-    print(f"mfcc-like: bf16 max|err|={err:.3e} (logit scale {scale_ref:.3f})")
-    assert err <= MAX_ABS * max(1.0, scale_ref)
-    assert np.mean(out.argmax(1) == ref.argmax(1)) >= MIN_TOP1
+    margin_check(out, ref, "mfcc-like res15")
+
+
+@pytest.mark.parametrize("name", ["res15", "res8"])
+def test_bf16_top1_margin_at_scale(name):
+    """1,024 MFCC-like clips on the bench's BatchNorm-calibrated model
+    (res15: C4's mode; res8: C3's).  Reference: the fp32 kernels (themselves within 2e-6
+    of the float64 oracle -- re-checked here on 16 clips); every clip outside 2 x the bf16
+    bound of a tie keeps its top-1."""
+    import bench
+    m = bench.bench_model(name, torch.device(DEV))
+    cfg = dict(ref_configs()[name])
+    g = torch.Generator(device=DEV)
+    g.manual_seed(21)
+    x = bench.mfcc_like(1024, DEV, g)
+    with torch.no_grad():
+        m.honk_precision = "f32"
+        ref = m(x).cpu().numpy().astype(np.float64)
+        m.honk_precision = "bf16"
+        out = m(x).cpu().numpy()
+    params = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    idx = np.arange(0, 1024, 64)
+    np.testing.assert_allclose(ref[idx], orc.forward(params, cfg, x[idx].cpu().numpy()), atol=1e-5, rtol=0)
+    margin_check(out, ref, f"{name} x 1024 calibrated")
 
 
 def test_bf16_batch_invariance(monkeypatch):
