@@ -320,7 +320,7 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
         act = H * W * CP * 2 * sp
         per_clip, layer = 0, 1
         for k in plan:
-            if k == "block16p_kernel":
+            if k in ("block16p_kernel", "block16k_kernel"):
                 per_clip += 3 * act
                 layer += 2
             elif k == "block16n_kernel":  # the whole stack: the conv0 output read once
@@ -332,6 +332,7 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
         dom = max(set(plan), key=plan.count)
         traffic = load_traffic(f"{dom}_{tag}", clips, model)
         what = {"block16p_kernel": "fused odd + even layer pair", "block16w_kernel": "weight-stationary layer",
+                "block16k_kernel": "fused odd + even layer pair, K split over two waves per SIMD",
                 "block16l_kernel": "last layer on the pair's streaming machinery, fused channel sums",
                 "block16r_kernel": "row-band layer",
                 "block16n_kernel": "every block layer of a clip, activations resident in LDS"}

@@ -213,7 +213,7 @@ def timing_read():
 
 # HONK_KERNEL_* of include/honk_hip.h
 KERNEL_NAMES = {1: "block_kernel", 2: "block16r_kernel", 3: "block16w_kernel", 4: "block16p_kernel",
-                5: "block16l_kernel", 6: "block16n_kernel"}
+                5: "block16l_kernel", 6: "block16n_kernel", 7: "block16k_kernel"}
 
 
 def res_launch_plan(desc, batch: int, n_cus: int = 0):

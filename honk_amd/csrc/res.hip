@@ -558,6 +558,7 @@ __global__ __launch_bounds__(256) void tail_sum_kernel(const float* __restrict__
 #include "res_bf16r.inc"
 #include "res_bf16w.inc"
 #include "res_bf16p.inc"
+#include "res_bf16k.inc"
 #include "res_bf16n.inc"
 
 // --------------------------------------------------------------------------- //
@@ -1213,6 +1214,7 @@ struct PairPlan {
   int padb;                            // f16x2: zero-column bytes each side of a slot's row
   int ns;                              // streams per workgroup (block16p_kernel NS)
   bool tbl;                            // bf16 two streams: the row-table instance (SCA = -1)
+  int ks;                              // 2: f16x2 with K split over two waves per SIMD (block16k_kernel)
 };
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i);
 static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
@@ -1238,8 +1240,8 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
 // class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
 static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int nstreams = 1, bool padcols = false,
-                          bool tbl = false) {
-  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams, tbl};
+                          bool tbl = false, int ks = 1) {
+  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams, tbl, ks};
   const int SP = sp_of(FM);
   const int P = 64, W = L.W, H = L.H;
   const long PXB = g16p_pxb(L.NT, SP);  // LDS pixel pitch
@@ -1312,8 +1314,9 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   if (F(-1) < 0) return pp;
   pp.NRA = (int)(nra > 2 ? nra : 2);
   pp.NRB = (int)(nrb > 2 ? nrb : 2);
-  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + g16p_lds_extra(FM == 2 || padcols || tbl, 4, pp.slotb) <=
-          g16p_lds_bytes() / nstreams;
+  const long extra = ks == 2 ? g16p_lds_extra(true, 8, pp.slotb) + g16k_xch_bytes()
+                             : g16p_lds_extra(FM == 2 || padcols || tbl, 4, pp.slotb);
+  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + extra <= g16p_lds_bytes() / nstreams;
   return pp;
 }
 
@@ -1335,7 +1338,7 @@ static bool pair_imm(const Layout& L, int FM, int dA, int dB) {
          (dA == 8 && dB == 8);
 }
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i) {
-  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1, false};
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1, false, 1};
   const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
@@ -1355,9 +1358,18 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
     const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, false, true);
     if (p2.ok && p2.ppr == 4 && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
   }
-  const PairPlan pp = plan_pair(L, FM, dA, sB, (int)cdiv(n, grid), 1, pair_imm(L, FM, dA, dB));
-  const int ppw = pair_ppw(SP, pp.ppr);
-  return pp.ok && ppw && pp.ppw <= ppw ? pp : no;
+  const bool imm = pair_imm(L, FM, dA, dB);
+  const int ppw = pair_ppw(SP, imm ? 4 : 0);
+  if (FM == 2 && imm && getenv("HONK_PAIR_KS") && getenv("HONK_PAIR_KS")[0] == '1') {
+    // opt-in: the K split over two waves per SIMD (block16k_kernel, res_bf16k.inc) -- measured
+    // 4-5 % slower than the one-wave pair (res15 f16x2 312K vs 327K clips/s, same box;
+    // DESIGN.md §3), so the default stays block16p_kernel
+    const PairPlan pk = plan_pair(L, FM, dA, sB, (int)cdiv(n, grid), 1, true, false, 2);
+    if (pk.ok && pk.ppr == 4 && pk.ppw <= ppw) return pk;
+  }
+  const PairPlan pp = plan_pair(L, FM, dA, sB, (int)cdiv(n, grid), 1, imm);
+  const int ppw1 = pair_ppw(SP, pp.ppr);
+  return pp.ok && ppw1 && pp.ppw <= ppw1 ? pp : no;
 }
 
 // The last layer on the pair machinery (block16l_kernel: layer A only, fused
@@ -1367,7 +1379,7 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
 // (no A-out ring: NRB = 1 unused slot, no lag).  HONK_LAST_KERNEL=w keeps the
 // weight-stationary kernel (the pair-vs-w bitwise tests).
 static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) {
-  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1, false};
+  const PairPlan no{false, 0, 0, 0, 0, 0, 0, 0, 1, false, 1};
   const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   const char* lenv = getenv("HONK_LAST_KERNEL");
@@ -1574,6 +1586,7 @@ bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd,
                     const Block16PArgs& pa);
 void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 void launch_pair2t_vf(dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
+bool launch_pairk_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 
 // flags (f16x2 only, may be null): [batch] the clips' admission flags (clip_scale_kernel,
 // tail_sum_kernel; honk_res_forward re-runs the flagged clips)
@@ -1662,8 +1675,11 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.ppr = pp.ppr;
             pa.padb = pp.padb;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
-            const dim3 gd(grid), bd(256 * pp.ns);
-            if (FM == 0 && pp.ns == 2) launch_pair2t_vf(gd, bd, st, pa);
+            const dim3 gd(grid), bd(256 * pp.ns * pp.ks);
+            if (pp.ks == 2) {
+              if (!launch_pairk_vf(dA, dil_of(d, i + 1), gd, bd, st, pa))
+                return fail(HONK_ERR_UNSUPPORTED, "block16k: no instance for dilations %d, %d", dA, dil_of(d, i + 1));
+            } else if (FM == 0 && pp.ns == 2) launch_pair2t_vf(gd, bd, st, pa);
             else if (!launch_pair_vf(FM, pp.ppr, pp.ppr == 4 && pp.padb > 0, dA, dil_of(d, i + 1), gd, bd, st, pa))
               return fail(HONK_ERR_UNSUPPORTED, "block16p: no tap-step instance for dilations %d, %d", dA,
                           dil_of(d, i + 1));
@@ -1825,8 +1841,9 @@ int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, i
     return cnt;
   }
   for (int i = 1; i <= L.L; ++i) {
-    if (pair_at(L, d, FM, n, grid, i).ok) {
-      put(HONK_KERNEL_PAIR);
+    const PairPlan pp = pair_at(L, d, FM, n, grid, i);
+    if (pp.ok) {
+      put(pp.ks == 2 ? HONK_KERNEL_PAIR_KS : HONK_KERNEL_PAIR);
       ++i;
     } else if (last_at(L, d, FM, i).ok) {
       put(HONK_KERNEL_LAST);

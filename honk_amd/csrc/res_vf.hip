@@ -50,6 +50,18 @@ void launch_pair2t_vf(dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) 
   hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2, 0, -1, -1>), gd, bd, 0, st, pa);
 }
 
+// f16x2 with the contraction split over two waves per SIMD (res_bf16k.inc)
+bool launch_pairk_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
+#define HONK_PK(a_, b_)                                                       \
+  if (dA == a_ && dB == b_) {                                                 \
+    hipLaunchKernelGGL((block16k_kernel<a_, b_>), gd, bd, 0, st, pa);        \
+    return true;                                                              \
+  }
+  HONK_PK(1, 1) HONK_PK(1, 2) HONK_PK(2, 2) HONK_PK(4, 4) HONK_PK(4, 8) HONK_PK(8, 8)
+#undef HONK_PK
+  return false;
+}
+
 // the last (odd) layer with its channel sums (dilation d)
 void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
   if (FM == 1) hipLaunchKernelGGL((block16l_kernel<3, 2, 9, 9, 2>), gd, bd, 0, st, pa);

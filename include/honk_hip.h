@@ -93,6 +93,7 @@ size_t honk_res_workspace_bytes(const honk_res_desc* d, int64_t batch);
 #define HONK_KERNEL_PAIR 4      /* fused odd + even layer pair (block16p_kernel)           */
 #define HONK_KERNEL_LAST 5      /* last (odd) layer, fused channel sums (block16l_kernel)  */
 #define HONK_KERNEL_NET 6       /* every block layer of a clip in LDS (block16n_kernel), bf16 */
+#define HONK_KERNEL_PAIR_KS 7   /* f16x2 pair, K split over two waves per SIMD (block16k_kernel) */
 int honk_res_launch_plan(const honk_res_desc* d, int64_t batch, int32_t n_cus, int32_t* kinds, int32_t max_kinds);
 /*
  * Pack a state_dict into kernel layout.  tensors[] (device, fp32, contiguous),

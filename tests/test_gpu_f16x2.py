@@ -112,14 +112,15 @@ PAIR_CASES = [("res15", {}, 600), ("res26", {}, 520), ("res8", {}, 700), ("res15
 
 @pytest.mark.parametrize("name,override,B", PAIR_CASES)
 def test_f16x2_pair_kernel_bitwise_vs_w(monkeypatch, name, override, B):
-    """The fused pair computes exactly what two weight-stationary launches compute
-    (same fp16 products, order and roundings)."""
+    """The one-wave fused pair (block16p_kernel; HONK_PAIR_KS=0) computes exactly what two
+    weight-stationary launches compute (same fp16 products, order and roundings)."""
     cfg = dict(ref_configs()[name])
     cfg.update(override)
     params, x = _res_case(cfg, B, seed=31)
     m = module(cfg, params, name)
     monkeypatch.setenv("HONK_RES_KERNEL", "p")
     monkeypatch.setenv("HONK_LAST_KERNEL", "w")
+    monkeypatch.setenv("HONK_PAIR_KS", "0")
     assert "block16p_kernel" in _native.res_launch_plan(m._desc(101, 40), B)
     outp = run(m, x)
     monkeypatch.setenv("HONK_RES_KERNEL", "w")
@@ -128,6 +129,31 @@ def test_f16x2_pair_kernel_bitwise_vs_w(monkeypatch, name, override, B):
     idx = list(range(0, B, max(1, B // 6)))[:6]
     tol = ATOL if name == "res15" and not override else POOLED_ATOL
     np.testing.assert_allclose(outp[idx], orc.forward(params, cfg, x[idx]), atol=tol, rtol=0)
+
+
+@pytest.mark.parametrize("B", [1, 3, 37, 300])
+def test_f16x2_ksplit_pair_vs_one_wave_pair(monkeypatch, B):
+    """block16k_kernel (HONK_PAIR_KS=1: the f16x2 pair with the contraction split over two
+    waves per SIMD, each output = half-0 partial + half-1 partial) against the one-wave pair
+    (the sequential 14-k-step sum): the same fp16 products, fp32 sums in another order,
+    which flips the fp16 rounding of a few stored activations -- logits within half the
+    1e-4 bar of each other, and each at the bar against the oracle."""
+    cfg = dict(ref_configs()["res15"])
+    params, x = _res_case(cfg, B, seed=41)
+    m = module(cfg, params, "res15")
+    monkeypatch.setenv("HONK_PAIR_KS", "1")  # opt-in (measured slower; DESIGN.md §3)
+    plan = _native.res_launch_plan(m._desc(101, 40), B)
+    assert plan == ["block16k_kernel"] * 6 + ["block16l_kernel"], plan
+    outk = run(m, x)
+    monkeypatch.setenv("HONK_PAIR_KS", "0")
+    assert _native.res_launch_plan(m._desc(101, 40), B)[0] == "block16p_kernel"
+    out1 = run(m, x)
+    idx = list(range(0, B, max(1, B // 4)))[:4]
+    ref = orc.forward(params, cfg, x[idx])
+    print(f"B={B}: |k-split - one-wave| max {np.abs(outk - out1).max():.2e}; vs oracle: k-split "
+          f"{np.abs(outk[idx] - ref).max():.2e}, one-wave {np.abs(out1[idx] - ref).max():.2e}")
+    np.testing.assert_allclose(outk, out1, atol=ATOL / 2, rtol=0)
+    np.testing.assert_allclose(outk[idx], ref, atol=ATOL, rtol=0)
 
 
 @pytest.mark.parametrize("name,override", [("res8", dict(n_feature_maps=1)), ("res8", dict(n_feature_maps=19)),

@@ -16,7 +16,7 @@ import os
 import sys
 from collections import defaultdict
 
-TAGS = ("block16p_kernel", "block16l_kernel", "conv0m_kernel", "tail_sum_kernel")
+TAGS = ("block16p_kernel", "block16k_kernel", "block16l_kernel", "conv0m_kernel", "tail_sum_kernel")
 
 
 def derive(m):
