@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
             s += relu_keepnan(acc);
           }
         v[u] = ((PH * PW > 1) ? s * inv : s) * cs;
-        if (ONES && c4 + u == C) v[u] = cs;
+        if (ONES && (c4 + u == C || c4 + u == C + 1)) v[u] = cs;
       }
       const f32x4 vv = {v[0], v[1], v[2], v[3]};
       store4(o + c4, vv);
@@ -499,6 +499,41 @@ __global__ __launch_bounds__(256) void tail_kernel(const float* __restrict__ x, 
     float acc = 0.f;
     for (int k = 0; k < C; ++k) acc = fmaf(wout[nlab * C + k], mean[k], acc);
     logits[(int64_t)b * NL + nlab] = acc + bout[nlab];
+  }
+}
+
+// The channel sums of a stored bf16 activation tensor [n][HW][CP] (CP = 48): the bf16
+// path's last layer when it is the B layer of a fused pair (an even last layer: res8,
+// res26), which stores its output like any pair.  One workgroup per clip: thread t sums
+// 16-B chunk t % 6 (8 channels) over pixels t / 6, t / 6 + 42, ... in order, then 48
+// threads add the 42 partials in order -- deterministic and independent of the clip's
+// position in the batch.  chsum[b][CP] is tail_sum_kernel's one partial per clip.
+__global__ __launch_bounds__(256) void act_chsum_kernel(const __bf16* __restrict__ act, float* __restrict__ chsum,
+                                                        int HW) {
+  constexpr int CP = 48, NCH = CP / 8, NPG = 256 / NCH;  // 6 chunks, 42 pixel groups
+  __shared__ float part[NPG][CP];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int j = t % NCH, pg = t / NCH;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (pg < NPG) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const u4* src = (const u4*)(act + (size_t)b * HW * CP) + j;
+    for (int p = pg; p < HW; p += NPG) {
+      const u4 v = src[(size_t)p * NCH];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[2 * e] += __builtin_bit_cast(float, v[e] << 16);
+        s[2 * e + 1] += __builtin_bit_cast(float, v[e] & 0xffff0000u);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[pg][8 * j + e] = s[e];
+  }
+  __syncthreads();
+  if (t < CP) {
+    float v = part[0][t];
+    for (int g = 1; g < NPG; ++g) v += part[g][t];
+    chsum[(size_t)b * CP + t] = v;
   }
 }
 
@@ -727,7 +762,7 @@ __global__ __launch_bounds__(256, 7) void conv0m_kernel(const float* __restrict_
           v = fmaf(fmaf(-q, (float)P, v), rp, q);
         }
         if constexpr (FM == 2) v *= cs;  // exact: a power of two
-        if (ONES && co16(NT, n, 4 * g + r) == C) v = cs;
+        if (ONES && (co16(NT, n, 4 * g + r) == C || co16(NT, n, 4 * g + r) == C + 1)) v = cs;
         hv[n][r] = (AT)v;
         if constexpr (SP == 2) lv[n][r] = (AT)(v - (float)hv[n][r]);
       }
@@ -1222,10 +1257,21 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
   // pairs fuse (the single weight-stationary layer is slower than the row-band one)
   // (measured: res15 bf16 +4 %; res8's 13-pixel rows lose 20 % -- row-band there);
   // f16x2: always (its only kernels)
+  // bf16 on rows < 32 pixels (res8, res26): only an even stack whose every layer pairs on
+  // the two-stream kernel (every pair and the last one; measured res8 0.128 ms per pair
+  // launch vs 2 x 0.070 row-band layers)
   bool want = FM == 2 || (L.NT == 3 && (FM == 1 || (L.W >= 32 && L.L >= 3 && pair_at(L, d, FM, 4096, 256, 1).ok)));
+  if (FM == 0 && L.NT == 3 && L.W < 32 && L.L >= 2 && L.L % 2 == 0) {
+    bool all = true;
+    for (int i = 1; i < L.L && all; i += 2) {
+      const PairPlan pp = pair_at(L, d, FM, 4096, 256, i);
+      all = pp.ok && pp.ns == 2;
+    }
+    want = want || all;
+  }
   if (const char* e = getenv("HONK_RES_KERNEL")) {
     if (e[0] == 'r' && FM != 2) return false;
-    if (e[0] == 'w') want = true;
+    if (e[0] == 'w' || e[0] == 'p') want = true;
   }
   if (!want) return false;
   if (L.W >= 64) return false;  // m-tile walk steps 64 pixels = at most one row carry
@@ -1316,7 +1362,10 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   pp.NRB = (int)(nrb > 2 ? nrb : 2);
   const long extra = ks == 2 ? g16p_lds_extra(true, 8, pp.slotb) + g16k_xch_bytes()
                              : g16p_lds_extra(FM == 2 || padcols || tbl, 4, pp.slotb);
-  pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + extra <= g16p_lds_bytes() / nstreams;
+  if (tbl && nstreams > 1)  // the streams share the zero block, sink and zeroed slot (block16p_body SHZ)
+    pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + 4 * g16p_tr() * g16p_teb() <= g16p_stream_bytes(nstreams, pp.slotb);
+  else
+    pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + extra <= g16p_lds_bytes() / nstreams;
   return pp;
 }
 
@@ -1342,7 +1391,9 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
   const int SP = sp_of(FM);
   const char* kenv = getenv("HONK_RES_KERNEL");
   if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
-  if (i % 2 == 0 || i + 1 >= L.L) return no;
+  // (bf16: B may be an even last layer -- it stores its output like any pair and
+  // act_chsum_kernel sums it; the other formats keep their fused last-layer sums)
+  if (i % 2 == 0 || i + 1 > L.L || (i + 1 == L.L && FM != 0)) return no;
   const int dA = dil_of(d, i), dB = dil_of(d, i + 1);
   const int sB = dB == dA ? 1 : (dB == 2 * dA ? 2 : 0);
   const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
@@ -1356,7 +1407,7 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
   // HONK_PAIR_STREAMS=1 selects those)
   if (FM == 0 && !(nse && nse[0] == '1')) {
     const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, false, true);
-    if (p2.ok && p2.ppr == 4 && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
+    if (p2.ok && (p2.ppr == 4 || p2.ppr == 2) && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
   }
   const bool imm = pair_imm(L, FM, dA, dB);
   const int ppw = pair_ppw(SP, imm ? 4 : 0);
@@ -1585,7 +1636,7 @@ static int launch_block16n(const Layout& L, const __bf16* in, const float* frb, 
 bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd, hipStream_t st,
                     const Block16PArgs& pa);
 void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
-void launch_pair2t_vf(dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
+void launch_pair2t_vf(int ppr, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 bool launch_pairk_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 
 // flags (f16x2 only, may be null): [batch] the clips' admission flags (clip_scale_kernel,
@@ -1648,11 +1699,13 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       if (rc) return rc;
       int grid = cu_count();
       if (grid > n) grid = (int)n;
+      bool last_stored = false;  // the last layer ran as a pair's B layer (act_chsum_kernel sums it)
       for (int i = 1; i <= L.L; ++i) {
         const bool even = (i % 2) == 0;
         {
           const PairPlan pp = pair_at(L, d, FM, n, grid, i);
           if (pp.ok) {
+            if (i + 1 == L.L) last_stored = true;
             const int dA = dil_of(d, i);
             const size_t cb = (size_t)n * L.H * L.W * L.CP * 2 * SP;
             Block16PArgs pa;
@@ -1679,7 +1732,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             if (pp.ks == 2) {
               if (!launch_pairk_vf(dA, dil_of(d, i + 1), gd, bd, st, pa))
                 return fail(HONK_ERR_UNSUPPORTED, "block16k: no instance for dilations %d, %d", dA, dil_of(d, i + 1));
-            } else if (FM == 0 && pp.ns == 2) launch_pair2t_vf(gd, bd, st, pa);
+            } else if (FM == 0 && pp.ns == 2) launch_pair2t_vf(pp.ppr, gd, bd, st, pa);
             else if (!launch_pair_vf(FM, pp.ppr, pp.ppr == 4 && pp.padb > 0, dA, dil_of(d, i + 1), gd, bd, st, pa))
               return fail(HONK_ERR_UNSUPPORTED, "block16p: no tap-step instance for dilations %d, %d", dA,
                           dil_of(d, i + 1));
@@ -1741,6 +1794,13 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         rc = dispatch_block16w(L.NT, FM, a, st);
         tl.done(st);
         if (rc) return rc;
+      }
+      if (last_stored) {
+        // the last layer was a pair's B layer (bf16): it stored its output in R
+        if (L.CP != 48 || SP != 1) return fail(HONK_ERR_UNSUPPORTED, "act_chsum_kernel: 48 bf16 channels only");
+        hipLaunchKernelGGL(act_chsum_kernel, dim3((unsigned)n), dim3(256), 0, st, R, chsum, L.H * L.W);
+        HONK_LAUNCH_CHECK("res act_chsum_kernel");
+        parts_last = 1;
       }
       const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,

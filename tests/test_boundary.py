@@ -278,7 +278,11 @@ def test_res_launch_plan_host_only(monkeypatch):
     assert plan("res8", "bf16x3") == ["block16p_kernel"] * 2 + ["block16w_kernel"] * 2
     assert plan("res15", "f32") == ["block_kernel"] * 13
     assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16l_kernel"]
-    assert plan("res8", "bf16") == ["block16r_kernel"] * 6  # 13-pixel rows: row-band measured faster
+    # 13- / 20-pixel rows, even stacks: every layer pairs on the two-stream kernel (the last
+    # pair's B layer stores its output, act_chsum_kernel sums it)
+    assert plan("res8", "bf16") == ["block16p_kernel"] * 3
+    assert plan("res26", "bf16") == ["block16p_kernel"] * 12
+    assert plan("res8", "bf16", n_layers=5) == ["block16r_kernel"] * 5  # odd stack: the row-band kernel
     assert plan("res26-narrow", "bf16") == ["block16r_kernel"] * 24
     assert plan("res15-narrow", "bf16x3") == ["block16r_kernel"] * 13
     monkeypatch.setenv("HONK_LAST_KERNEL", "w")
@@ -291,6 +295,9 @@ def test_res_launch_plan_host_only(monkeypatch):
     monkeypatch.setenv("HONK_RES_KERNEL", "n")  # the whole-stack kernel (opt-in)
     assert plan("res8", "bf16") == ["block16n_kernel"]
     assert plan("res8-narrow", "bf16") == ["block16n_kernel"]
+    monkeypatch.setenv("HONK_RES_KERNEL", "r")
+    assert plan("res8", "bf16") == ["block16r_kernel"] * 6
+    monkeypatch.setenv("HONK_RES_KERNEL", "n")
     assert plan("res26-narrow", "bf16") == ["block16r_kernel"] * 24  # 50 x 20 maps: no room for three images
     assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16l_kernel"]  # dilated: not taken
 

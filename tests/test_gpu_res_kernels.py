@@ -107,8 +107,9 @@ def test_rowband_last_residual_layer_bf16_tight(monkeypatch, name):
     spill listing shows spilling (whole tuples, tools/check_spills.py).  A stale dword of
     a reloaded operand would move the logits by O(1); the row-band bf16 path must stay at
     bf16's own rounding against the reference's golden logits: <= 5e-3 (measured <= 2e-3)
-    and the same top-1, with the launch plan confirming the kernel ran."""
-    monkeypatch.delenv("HONK_RES_KERNEL", raising=False)
+    and the same top-1, with the launch plan confirming the kernel ran.  (res8's default
+    is now the two-stream pair path, test_res8_bf16_pairs_default below: r forces this one.)"""
+    monkeypatch.setenv("HONK_RES_KERNEL", "r")
     cfg, params, x, logits, meta = load_fixture(name)
     m = _module(cfg, params, meta["model"], "bf16")
     assert _native.res_launch_plan(m._desc(101, 40), len(x)) == ["block16r_kernel"] * cfg["n_layers"]
@@ -117,6 +118,35 @@ def test_rowband_last_residual_layer_bf16_tight(monkeypatch, name):
     print(f"{name}: bf16 row-band max|err| vs reference = {err:.2e}")
     assert err <= 5e-3
     assert (out.argmax(1) == logits.argmax(1)).all()
+
+
+@pytest.mark.parametrize("name", ["res8", "res8-b5"])
+def test_res8_bf16_pairs_default(monkeypatch, name):
+    """C3's default path (round 6): res8's six layers as three fused pairs on the
+    two-stream row-table kernel (block16p_kernel<3, 1, 2, 5, 2, 0, -1, -1>: 13-pixel rows,
+    2-KiB ring slots, the zero block / sink / zeroed slot shared by the streams), the last
+    pair's B layer storing its output and act_chsum_kernel summing it per clip.  The bar of
+    the row-band test above (<= 5e-3 vs the reference's golden logits, the same top-1), and
+    the logits bitwise invariant to batch composition (a clip alone, in a batch, at another
+    position)."""
+    monkeypatch.delenv("HONK_RES_KERNEL", raising=False)
+    cfg, params, x, logits, meta = load_fixture(name)
+    m = _module(cfg, params, meta["model"], "bf16")
+    assert _native.res_launch_plan(m._desc(101, 40), len(x)) == ["block16p_kernel"] * 3
+    out = _run(m, x)
+    err = float(np.abs(out - logits).max())
+    print(f"{name}: bf16 pairs max|err| vs reference = {err:.2e}")
+    assert err <= 5e-3
+    assert (out.argmax(1) == logits.argmax(1)).all()
+    one = _run(m, x[1:2])
+    rev = _run(m, x[::-1].copy())
+    assert np.array_equal(one[0], out[1])
+    assert np.array_equal(rev[::-1], out)
+    # a batch of many clips per stream (multi-clip streams, every workgroup busy)
+    rng = np.random.Generator(np.random.PCG64(3))
+    big = np.concatenate([rng.standard_normal((700, 101, 40)).astype(np.float32), x])
+    outb = _run(m, big)
+    assert np.array_equal(outb[700:], out)
 
 
 # multi-clip streams per workgroup (batches above the CU count), pooled widths,
@@ -132,7 +162,10 @@ def test_pair_kernel_bitwise_vs_w(monkeypatch, name, override, B, prec):
     cfg = dict(ref_configs()[name])
     cfg.update(override)
     if prec == "bf16" and "res_pool" in cfg:
-        pytest.skip("bf16 pairs run on full-width (40-pixel) rows only; pooled bf16 stays on the row-band kernel")
+        # pooled bf16 (13- / 20-pixel rows) pairs on the two-stream kernel; an odd stack keeps
+        # its last layer on the weight-stationary kernel (an even one's last pair stores its
+        # output and act_chsum_kernel sums it: not the w kernel's fused fp32 sums)
+        cfg["n_layers"] = 5
     params, x = _case(cfg, B, seed=31)
     m = _module(cfg, params, name, prec)
     monkeypatch.setenv("HONK_RES_KERNEL", "p")
