@@ -502,16 +502,19 @@ __global__ __launch_bounds__(256) void tail_kernel(const float* __restrict__ x, 
   }
 }
 
-// The channel sums of a stored bf16 activation tensor [n][HW][CP] (CP = 48): the bf16
-// path's last layer when it is the B layer of a fused pair (an even last layer: res8,
-// res26), which stores its output like any pair.  One workgroup per clip: thread t sums
-// 16-B chunk t % 6 (8 channels) over pixels t / 6, t / 6 + 42, ... in order, then 48
-// threads add the 42 partials in order -- deterministic and independent of the clip's
-// position in the batch.  chsum[b][CP] is tail_sum_kernel's one partial per clip.
-__global__ __launch_bounds__(256) void act_chsum_kernel(const __bf16* __restrict__ act, float* __restrict__ chsum,
-                                                        int HW) {
+// The head over a stored bf16 activation tensor [n][HW][CP] (CP = 48): the bf16 path's
+// last layer when it is the B layer of a fused pair (an even last layer: res8, res26),
+// which stores its output like any pair.  One workgroup per clip: thread t sums 16-B chunk
+// t % 6 (8 channels) over pixels t / 6, t / 6 + 42, ... in order, 48 threads add the 42
+// partials in order (deterministic, independent of the clip's position in the batch), then
+// tail_sum_kernel's last BatchNorm on the channel means and the Linear.
+__global__ __launch_bounds__(256) void tail_act_kernel(const __bf16* __restrict__ act, const float* __restrict__ wout,
+                                                       const float* __restrict__ bout, float* __restrict__ logits,
+                                                       int HW, int C, int NL, const float* __restrict__ bn_scale,
+                                                       const float* __restrict__ bn_shift) {
   constexpr int CP = 48, NCH = CP / 8, NPG = 256 / NCH;  // 6 chunks, 42 pixel groups
   __shared__ float part[NPG][CP];
+  __shared__ float mean[CP];
   const int b = blockIdx.x, t = threadIdx.x;
   const int j = t % NCH, pg = t / NCH;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -533,7 +536,13 @@ __global__ __launch_bounds__(256) void act_chsum_kernel(const __bf16* __restrict
   if (t < CP) {
     float v = part[0][t];
     for (int g = 1; g < NPG; ++g) v += part[g][t];
-    chsum[(size_t)b * CP + t] = v;
+    mean[t] = bn_scale ? fmaf(v / (float)HW, bn_scale[t], bn_shift[t]) : v / (float)HW;
+  }
+  __syncthreads();
+  for (int n = t; n < NL; n += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < C; ++k) acc = fmaf(wout[n * C + k], mean[k], acc);
+    logits[(int64_t)b * NL + n] = acc + bout[n];
   }
 }
 
@@ -776,6 +785,141 @@ __global__ __launch_bounds__(256, 7) void conv0m_kernel(const float* __restrict_
       }
       if constexpr (NT & 1) *(u32x2*)(op + pt * CP * 2 + 64 * (NT / 2) + 8 * g) = __builtin_bit_cast(u32x2, vv[NT - 1]);
     }
+  }
+}
+
+// --------------------------------------------------------------------------- //
+// conv0 of the bf16 format (FM 0) with an average pool (res8 4x3, res26 2x2; round 6).
+// bf16 weights (the format's own) times the input as bf16 (hi, lo): two products, in a K
+// layout all four lane groups share -- slot j of lane group g reads plane (g < 2: hi, else
+// lo) at tap row dy = 2 (g & 1) + j / 4 and tap column dx = j % 4 (dy or dx = 3: a zero
+// weight; the read is an in-image value or the zero border, and a non-finite one only
+// lands in a clip whose logits are NaN anyway).  A lane's B operand for pool member (mr,
+// mc) is then 4 pairs of ONE plane: patch rows mr, mr + 1, columns mc, mc + 2 (and + 1),
+// counted from its window's row 4 ph + 2 (g & 1) -- the same registers in every lane group.
+// So an m-tile loads its lane's (PH + 1) x (PW + 3) patch once (res8: 30 LDS reads per 16
+// pooled outputs; conv0m_kernel reads 8 u16 per member, 96) and packs each row's pairs once
+// (25 packs; conv0m_kernel: 48).  Everything else is conv0m_kernel's.
+template <int NT, int PH, int PW, bool ONES, int FWB = 0>
+__global__ __launch_bounds__(256, 6) void conv0p_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
+                                                     const float* __restrict__ w0, int Hin, int Win, int H, int W,
+                                                     int C) {
+  constexpr int CP = 16 * NT, CB = CP * 2;
+  constexpr int PR = PH + 1, PC = PW + 3;  // patch rows, columns (pairs per row: PC - 1)
+  extern __shared__ __attribute__((aligned(16))) unsigned short c0lds[];  // hi plane, lo plane, a zero row
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int clip = blockIdx.x;
+  const int Wb = FWB > 0 ? FWB : Win + 2, plane = (Hin + 2) * Wb;
+  unsigned short* hp = c0lds;
+  unsigned short* lp = c0lds + plane;
+
+  // weights: A fragment of n-tile n (row = out channel co16(NT, n, i16), k-chunk g)
+  u32x4 wa[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int co = co16(NT, n, i16);
+    unsigned short v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int dy = 2 * (g & 1) + j / 4, dx = j % 4;
+      const float w = w0[co * 9 + (dy < 3 && dx < 3 ? dy * 3 + dx : 0)];
+      v[j] = __builtin_bit_cast(unsigned short, (__bf16)(dy < 3 && dx < 3 ? w : 0.f));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wa[n][j] = (unsigned)v[2 * j] | ((unsigned)v[2 * j + 1] << 16);
+  }
+
+  // stage the clip (conv0m_kernel's staging), plus one zero row past the lo plane: the
+  // patch of the last pooled row reaches one row beyond the bordered image when PH | Hin
+  const float* xc = x + (size_t)clip * Hin * Win;
+  {
+    const int n16 = ((2 * plane + Wb) * 2 + 15) / 16;
+    for (int i = threadIdx.x; i < n16; i += 256) ((u32x4*)c0lds)[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+  auto put = [&](int r, int c, float v) {
+    const int i = (r + 1) * Wb + c + 1;
+    const __bf16 h = (__bf16)v;
+    hp[i] = __builtin_bit_cast(unsigned short, h);
+    lp[i] = __builtin_bit_cast(unsigned short, (__bf16)(v - (float)h));
+  };
+  if ((Win & 3) == 0) {
+    const int w4 = Win >> 2, n4 = Hin * w4;
+    for (int i = threadIdx.x; i < n4; i += 256) {
+      const int r = i / w4, c = (i - r * w4) * 4;
+      const f32x4 v = *(const f32x4*)(xc + (size_t)r * Win + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) put(r, c + u, v[u]);
+    }
+  } else {
+    for (int i = threadIdx.x; i < Hin * Win; i += 256) {
+      const int r = i / Win;
+      put(r, i - r * Win, xc[i]);
+    }
+  }
+  __syncthreads();
+
+  const int npo = H * W;
+  const int ngroups = (npo + 15) >> 4;
+  char* oc = (char*)out + (size_t)clip * npo * CB;
+  for (int gi = wave; gi < ngroups; gi += 4) {
+    const int q0 = 16 * gi + i16;
+    const int q = q0 < npo ? q0 : npo - 1;
+    const int ph = q / W, pw = q - ph * W;
+    const unsigned short* pb = c0lds + (g >= 2 ? plane : 0) + (ph * PH + 2 * (g & 1)) * Wb + pw * PW;
+    // the patch's pairs: pr[i][c] = (row i column c, row i column c + 1)
+    unsigned pr[PR][PC - 1];
+#pragma unroll
+    for (int i = 0; i < PR; ++i) {
+      unsigned short v[PC];
+#pragma unroll
+      for (int c = 0; c < PC; ++c) v[c] = pb[i * Wb + c];
+#pragma unroll
+      for (int c = 0; c < PC - 1; ++c) pr[i][c] = (unsigned)v[c] | ((unsigned)v[c + 1] << 16);
+    }
+    f32x4 pacc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) pacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto member = [&](auto kc) {
+      constexpr int k = decltype(kc)::value, mr = k / PW, mc = k % PW;
+      const u32x4 b{pr[mr][mc], pr[mr][mc + 2], pr[mr + 1][mc], pr[mr + 1][mc + 2]};
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[n]),
+                                                                  __builtin_bit_cast(bf16x8, b),
+                                                                  f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pacc[n][r] += relu_keepnan(acc[r]);
+      }
+      if constexpr (k & 1) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) asm volatile("" : "+v"(pacc[n]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    static_for<PH * PW>(member);
+    if (q0 >= npo) continue;
+    char* op = oc + (size_t)q0 * CB;
+    typename ActT<0>::V4 hv[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = pacc[n][r];
+        constexpr float rp = 1.0f / (float)(PH * PW);
+        const float qv = v * rp;
+        v = fmaf(fmaf(-qv, (float)(PH * PW), v), rp, qv);
+        const int co = co16(NT, n, 4 * g + r);
+        if (ONES && (co == C || co == C + 1)) v = 1.f;
+        hv[n][r] = (__bf16)v;
+      }
+#pragma unroll
+    for (int p2 = 0; p2 < NT / 2; ++p2) {
+      const u32x2 a0 = __builtin_bit_cast(u32x2, hv[2 * p2]), a1 = __builtin_bit_cast(u32x2, hv[2 * p2 + 1]);
+      *(u32x4*)(op + 64 * p2 + 16 * g) = u32x4{a0[0], a0[1], a1[0], a1[1]};
+    }
+    if constexpr (NT & 1) *(u32x2*)(op + 64 * (NT / 2) + 8 * g) = __builtin_bit_cast(u32x2, hv[NT - 1]);
   }
 }
 
@@ -1392,7 +1536,7 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
   const char* kenv = getenv("HONK_RES_KERNEL");
   if (L.NT != 3 || (kenv && (kenv[0] == 'w' || kenv[0] == 'r'))) return no;
   // (bf16: B may be an even last layer -- it stores its output like any pair and
-  // act_chsum_kernel sums it; the other formats keep their fused last-layer sums)
+  // tail_act_kernel sums it; the other formats keep their fused last-layer sums)
   if (i % 2 == 0 || i + 1 > L.L || (i + 1 == L.L && FM != 0)) return no;
   const int dA = dil_of(d, i), dB = dil_of(d, i + 1);
   const int sB = dB == dA ? 1 : (dB == 2 * dA ? 2 : 0);
@@ -1557,6 +1701,29 @@ template <int NT, int FM, bool ONES>
 static int launch_conv0m_nt(const Layout& L, const float* x, void* out, const float* w0, int64_t n,
                             hipStream_t st, const float* cscale) {
   const unsigned lds = 2u * (unsigned)((L.Hin + 2) * (L.Win + 2)) * 2u;
+  // bf16 with a pool: the shared-layout patch kernel (conv0p_kernel); HONK_CONV0=m keeps conv0m_kernel
+  const char* ce = getenv("HONK_CONV0");
+  if constexpr (FM == 0) {
+    if (L.ph * L.pw > 1 && !(ce && ce[0] == 'm')) {
+      const unsigned ldsp = lds + 2u * (unsigned)(L.Win + 2);
+#define HONK_C0P(ph_, pw_)                                                                                     \
+  if (L.ph == ph_ && L.pw == pw_) {                                                                            \
+    if (ldsp > 65536)                                                                                          \
+      (void)hipFuncSetAttribute((const void*)conv0p_kernel<NT, ph_, pw_, ONES>,                               \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsp);                      \
+    if (L.Win == 40)                                                                                           \
+      hipLaunchKernelGGL((conv0p_kernel<NT, ph_, pw_, ONES, 42>), dim3((unsigned)n), dim3(256), ldsp, st, x,   \
+                         (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C);                                      \
+    else                                                                                                       \
+      hipLaunchKernelGGL((conv0p_kernel<NT, ph_, pw_, ONES>), dim3((unsigned)n), dim3(256), ldsp, st, x,       \
+                         (__bf16*)out, w0, L.Hin, L.Win, L.H, L.W, L.C);                                      \
+    HONK_LAUNCH_CHECK("res conv0p_kernel");                                                                    \
+    return HONK_OK;                                                                                            \
+  }
+      HONK_C0P(2, 2) HONK_C0P(4, 3)
+#undef HONK_C0P
+    }
+  }
 #define HONK_C0M(ph_, pw_)                                                                              \
   if (L.ph == ph_ && L.pw == pw_) {                                                                     \
     if (lds > 65536)                                                                                    \
@@ -1580,7 +1747,7 @@ static int launch_conv0_16(const Layout& L, const float* x, void* out, const flo
                            const float* cscale = nullptr) {
   const char* e = getenv("HONK_CONV0");
   const bool valu = e && e[0] == 'v';
-  const bool fits = 2L * (L.Hin + 2) * (L.Win + 2) * 2 <= 160 * 1024 && n <= 0x7fffffff;
+  const bool fits = 2L * (L.Hin + 3) * (L.Win + 2) * 2 <= 160 * 1024 && n <= 0x7fffffff;
   if (!valu && fits) {
     int rc = 1;
     if (L.NT == 1) rc = launch_conv0m_nt<1, FM, ONES>(L, x, out, w0, n, st, cscale);
@@ -1699,7 +1866,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
       if (rc) return rc;
       int grid = cu_count();
       if (grid > n) grid = (int)n;
-      bool last_stored = false;  // the last layer ran as a pair's B layer (act_chsum_kernel sums it)
+      bool last_stored = false;  // the last layer ran as a pair's B layer (tail_act_kernel sums it)
       for (int i = 1; i <= L.L; ++i) {
         const bool even = (i % 2) == 0;
         {
@@ -1795,14 +1962,15 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
         tl.done(st);
         if (rc) return rc;
       }
+      const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       if (last_stored) {
         // the last layer was a pair's B layer (bf16): it stored its output in R
-        if (L.CP != 48 || SP != 1) return fail(HONK_ERR_UNSUPPORTED, "act_chsum_kernel: 48 bf16 channels only");
-        hipLaunchKernelGGL(act_chsum_kernel, dim3((unsigned)n), dim3(256), 0, st, R, chsum, L.H * L.W);
-        HONK_LAUNCH_CHECK("res act_chsum_kernel");
-        parts_last = 1;
+        if (L.CP != 48 || SP != 1) return fail(HONK_ERR_UNSUPPORTED, "tail_act_kernel: 48 bf16 channels only");
+        hipLaunchKernelGGL(tail_act_kernel, dim3((unsigned)n), dim3(256), 0, st, R, packed + L.off_wout,
+                           packed + L.off_bout, logits + c0 * L.NL, L.H * L.W, L.C, L.NL, bn_last, bn_last + L.CP);
+        HONK_LAUNCH_CHECK("res tail_act_kernel");
+        continue;
       }
-      const float* bn_last = packed + L.off_bn + (size_t)2 * L.CP * (L.L - 1);
       hipLaunchKernelGGL(tail_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, chsum, packed + L.off_wout,
                          packed + L.off_bout, logits + c0 * L.NL, parts_last, L.H * L.W, L.C, L.CP, L.NL,
                          bn_last, bn_last + L.CP, tail_cs, packed + L.off_range + HONK_NUM_OUT_SCALE,

@@ -279,7 +279,7 @@ def test_res_launch_plan_host_only(monkeypatch):
     assert plan("res15", "f32") == ["block_kernel"] * 13
     assert plan("res15", "bf16") == ["block16p_kernel"] * 6 + ["block16l_kernel"]
     # 13- / 20-pixel rows, even stacks: every layer pairs on the two-stream kernel (the last
-    # pair's B layer stores its output, act_chsum_kernel sums it)
+    # pair's B layer stores its output, tail_act_kernel sums it)
     assert plan("res8", "bf16") == ["block16p_kernel"] * 3
     assert plan("res26", "bf16") == ["block16p_kernel"] * 12
     assert plan("res8", "bf16", n_layers=5) == ["block16r_kernel"] * 5  # odd stack: the row-band kernel
