@@ -1394,6 +1394,7 @@ struct PairPlan {
   int ns;                              // streams per workgroup (block16p_kernel NS)
   bool tbl;                            // bf16 two streams: the row-table instance (SCA = -1)
   int ks;                              // 2: f16x2 with K split over two waves per SIMD (block16k_kernel)
+  bool lin;                            // bf16 two streams, undilated A: linear A-in DMA (block16p_body LIN)
 };
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i);
 static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
@@ -1430,8 +1431,8 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
 // class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
 static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int nstreams = 1, bool padcols = false,
-                          bool tbl = false, int ks = 1) {
-  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams, tbl, ks};
+                          bool tbl = false, int ks = 1, bool lin = false) {
+  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams, tbl, ks, lin};
   const int SP = sp_of(FM);
   const int P = 64, W = L.W, H = L.H;
   const long PXB = g16p_pxb(L.NT, SP);  // LDS pixel pitch
@@ -1439,6 +1440,7 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   // slot pitch: room for the DMA's whole pieces, = W * PXB mod 256 so that
   // stream pixels stay at a constant LDS pitch across a row change
   pp.slotb = (int)(W * PXB + ((pp.ppr * 1024 - W * PXB + 255) / 256) * 256);
+  if (lin) pp.slotb = (int)(W * PXB);  // rows contiguous in the ring (block16p_body LIN)
   if (FM == 2 && padcols) {
     // f16x2 last layer (res_bf16p.inc PADC): zero columns either side of every slot's
     // row, at least the widest tap offset (B's sB d columns), in 256-B units; the DMA's
@@ -1503,6 +1505,23 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   pp.ppw = (int)((maxrows * pp.ppr + 1) / 2);
   if (F(-1) < 0) return pp;
   pp.NRA = (int)(nra > 2 ? nra : 2);
+  if (lin) {
+    // a ring of whole 1-KiB pieces: NRA a multiple of 1024 / gcd(slot, 1024); the pieces per
+    // step from the bytes of rows 0 .. F(k)
+    int g = 1024;
+    for (int b = pp.slotb; b % 2 == 0 && g > 1; b /= 2) g /= 2;  // 1024 / gcd(slotb, 1024)
+    pp.NRA = ((int)nra + 1 + g - 1) / g * g;  // (+1: a step's last piece may start the row after F(k))
+    const long ptot = (rows_total * (long)pp.slotb + 1023) / 1024;
+    auto pieces = [&](long k) {
+      const long p = ((F(k) + 1) * (long)pp.slotb + 1023) / 1024;
+      return p < ptot ? p : ptot;
+    };
+    long mx = 0;
+    for (long k = 0; k < ns; ++k)
+      if (pieces(k) - pieces(k - 1) > mx) mx = pieces(k) - pieces(k - 1);
+    pp.ppw = (int)((mx + 1) / 2);
+    if ((long)pp.NRA * pp.slotb / 1024 <= 2 * pp.ppw + pieces(-1)) return pp;  // (the ring must outrun a step)
+  }
   pp.NRB = (int)(nrb > 2 ? nrb : 2);
   const long extra = ks == 2 ? g16p_lds_extra(true, 8, pp.slotb) + g16k_xch_bytes()
                              : g16p_lds_extra(FM == 2 || padcols || tbl, 4, pp.slotb);
@@ -1550,6 +1569,13 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
   // its step loop, now removed), 416K with one stream on the tap-step instances, same box;
   // HONK_PAIR_STREAMS=1 selects those)
   if (FM == 0 && !(nse && nse[0] == '1')) {
+    // undilated A on narrow rows whose LDS pixel is the HBM pixel: the linear A-in DMA
+    // (HONK_PAIR_LIN=0 keeps the row pieces)
+    const char* le = getenv("HONK_PAIR_LIN");
+    if (dA == 1 && g16p_pxb(3, SP) == 32 * 3 * SP && L.W < 32 && !(le && le[0] == '0')) {
+      const PairPlan pl = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, false, true, 1, true);
+      if (pl.ok && pl.ppr == 2 && pl.ppw <= 4) return pl;
+    }
     const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, false, true);
     if (p2.ok && (p2.ppr == 4 || p2.ppr == 2) && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
   }
@@ -1803,7 +1829,7 @@ static int launch_block16n(const Layout& L, const __bf16* in, const float* frb, 
 bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd, hipStream_t st,
                     const Block16PArgs& pa);
 void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
-void launch_pair2t_vf(int ppr, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
+void launch_pair2t_vf(int ppr, bool lin, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 bool launch_pairk_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 
 // flags (f16x2 only, may be null): [batch] the clips' admission flags (clip_scale_kernel,
@@ -1899,7 +1925,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             if (pp.ks == 2) {
               if (!launch_pairk_vf(dA, dil_of(d, i + 1), gd, bd, st, pa))
                 return fail(HONK_ERR_UNSUPPORTED, "block16k: no instance for dilations %d, %d", dA, dil_of(d, i + 1));
-            } else if (FM == 0 && pp.ns == 2) launch_pair2t_vf(pp.ppr, gd, bd, st, pa);
+            } else if (FM == 0 && pp.ns == 2) launch_pair2t_vf(pp.ppr, pp.lin, gd, bd, st, pa);
             else if (!launch_pair_vf(FM, pp.ppr, pp.ppr == 4 && pp.padb > 0, dA, dil_of(d, i + 1), gd, bd, st, pa))
               return fail(HONK_ERR_UNSUPPORTED, "block16p: no tap-step instance for dilations %d, %d", dA,
                           dil_of(d, i + 1));

@@ -46,9 +46,10 @@ bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd,
 
 // bf16, two streams per workgroup on the row-table walk (SCA = -1: no tap-step
 // immediates -- the two streams' rings leave no room for pad columns); ppr 4: 40-pixel
-// rows (res15), 2: 13..21-pixel rows (res8, res26)
-void launch_pair2t_vf(int ppr, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
-  if (ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2, 0, -1, -1>), gd, bd, 0, st, pa);
+// rows (res15), 2: 13..21-pixel rows (res8, res26); lin: their linear A-in DMA
+void launch_pair2t_vf(int ppr, bool lin, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
+  if (lin) hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 4, 2, 0, -1, -1, true>), gd, bd, 0, st, pa);
+  else if (ppr == 4) hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2, 0, -1, -1>), gd, bd, 0, st, pa);
   else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 2, 0, -1, -1>), gd, bd, 0, st, pa);
 }
 
