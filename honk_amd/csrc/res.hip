@@ -801,7 +801,7 @@ __global__ __launch_bounds__(256, 7) void conv0m_kernel(const float* __restrict_
 // pooled outputs; conv0m_kernel reads 8 u16 per member, 96) and packs each row's pairs once
 // (25 packs; conv0m_kernel: 48).  Everything else is conv0m_kernel's.
 template <int NT, int PH, int PW, bool ONES, int FWB = 0>
-__global__ __launch_bounds__(256, 6) void conv0p_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
+__global__ __launch_bounds__(256, 5) void conv0p_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
                                                      const float* __restrict__ w0, int Hin, int Win, int H, int W,
                                                      int C) {
   constexpr int CP = 16 * NT, CB = CP * 2;
@@ -866,7 +866,9 @@ __global__ __launch_bounds__(256, 6) void conv0p_kernel(const float* __restrict_
   for (int gi = wave; gi < ngroups; gi += 4) {
     const int q0 = 16 * gi + i16;
     const int q = q0 < npo ? q0 : npo - 1;
-    const int ph = q / W, pw = q - ph * W;
+    // (FWB > 0: the pooled width (FWB - 2) / PW is a compile-time divisor)
+    const int Wq = FWB > 0 ? (FWB - 2) / PW : W;
+    const int ph = q / Wq, pw = q - ph * Wq;
     const unsigned short* pb = c0lds + (g >= 2 ? plane : 0) + (ph * PH + 2 * (g & 1)) * Wb + pw * PW;
     // the patch's pairs: pr[i][c] = (row i column c, row i column c + 1)
     unsigned pr[PR][PC - 1];
@@ -881,24 +883,36 @@ __global__ __launch_bounds__(256, 6) void conv0p_kernel(const float* __restrict_
     f32x4 pacc[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) pacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto member = [&](auto kc) {
+    // software-pipelined members: member k + 1's MFMAs issue before member k's ReLU + sum
+    // reads its results (SQ: 52 % of the wave cycles stalled on an instruction dependency
+    // when each member's VALU read its MFMAs right behind them)
+    f32x4 am[2][NT];
+    auto issue = [&](auto kc) {
       constexpr int k = decltype(kc)::value, mr = k / PW, mc = k % PW;
       const u32x4 b{pr[mr][mc], pr[mr][mc + 2], pr[mr + 1][mc], pr[mr + 1][mc + 2]};
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[n]),
-                                                                  __builtin_bit_cast(bf16x8, b),
-                                                                  f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pacc[n][r] += relu_keepnan(acc[r]);
-      }
-      if constexpr (k & 1) {
-#pragma unroll
-        for (int n = 0; n < NT; ++n) asm volatile("" : "+v"(pacc[n]));
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      for (int n = 0; n < NT; ++n)
+        am[k & 1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[n]),
+                                                              __builtin_bit_cast(bf16x8, b),
+                                                              f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     };
-    static_for<PH * PW>(member);
+    auto fold = [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pacc[n][r] += relu_keepnan(am[k & 1][n][r]);
+    };
+    issue(std::integral_constant<int, 0>{});
+    static_for<PH * PW>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (k + 1 < PH * PW) issue(std::integral_constant<int, k + 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+      fold(kc);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) asm volatile("" : "+v"(pacc[n]));
+      __builtin_amdgcn_sched_barrier(0);
+    });
     if (q0 >= npo) continue;
     char* op = oc + (size_t)q0 * CB;
     typename ActT<0>::V4 hv[NT];
