@@ -95,6 +95,9 @@ _PROTOS = {
                                              ctypes.c_void_p]),
     "honk_res_tail_bwd_f32": (ctypes.c_int, [c_f32p] * 7 + [ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
                                              ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "honk_bn_count_scale": (ctypes.c_int, [ctypes.c_double]),
+    "honk_bn_partials_f32": (ctypes.c_int, [c_f32p, c_f32p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64,
+                                            ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p]),
     "honk_conv3x3_stats_bytes": (ctypes.c_size_t, [ctypes.c_int64] + [ctypes.c_int32] * 4),
     "honk_conv3x3_stats_f32": (ctypes.c_int, [c_f32p] * 3 + [ctypes.c_int64] + [ctypes.c_int32] * 6
                                + [c_f32p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),

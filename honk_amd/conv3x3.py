@@ -16,11 +16,13 @@ loop (train.py:131-134) runs unchanged.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
 
 from honk_amd import _native
+from honk_amd import syncbn
 
 CHANNELS = (19, 45)
 
@@ -328,9 +330,11 @@ class _ResTail(torch.autograd.Function):
             buf, d = box.pop("fwd")
             # fold: no y -- the next conv reads (s - mean) * invstd from s (box["fold"]);
             # the returned y is a placeholder of its shape that nothing reads
-            _native.check(_native.load().honk_res_tail_fwd_s_f32(
-                h.data_ptr(), None if fold else y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
-                ptr(running_var), buf.data_ptr(), B, C, H, W, d, momentum, eps, st), "honk_res_tail_fwd_s_f32")
+            with _synced(buf):
+                _native.check(_native.load().honk_res_tail_fwd_s_f32(
+                    h.data_ptr(), None if fold else y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                    ptr(running_mean), ptr(running_var), buf.data_ptr(), B, C, H, W, d, momentum, eps, st),
+                    "honk_res_tail_fwd_s_f32")
             if fold:
                 box["fold"] = (h, mean, invstd)
                 ctx.save_for_backward(mask, h, invstd, mean)
@@ -347,10 +351,15 @@ class _ResTail(torch.autograd.Function):
         if box is not None and "fwd" in box:
             STATS_USED["fwd"] += 1
             buf, d = box.pop("fwd")
-            _native.check(_native.load().honk_res_tail_fwd_part_f32(
-                h.data_ptr(), ptr(old), ptr(s), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
-                ptr(running_var), buf.data_ptr(), B, C, H, W, d, momentum, eps, st), "honk_res_tail_fwd_part_f32")
+            with _synced(buf):
+                _native.check(_native.load().honk_res_tail_fwd_part_f32(
+                    h.data_ptr(), ptr(old), ptr(s), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                    ptr(running_mean), ptr(running_var), buf.data_ptr(), B, C, H, W, d, momentum, eps, st),
+                    "honk_res_tail_fwd_part_f32")
         else:
+            if syncbn.active():
+                raise RuntimeError("honk_amd: SyncBN needs the conv epilogue's statistics (model.py routes "
+                                   "other shapes to syncbn.batch_norm)")
             ws, nb = _bn_ws(B, C, H * W, h.device)
             _native.check(_native.load().honk_res_tail_fwd_f32(h.data_ptr(), ptr(old), ptr(s), y.data_ptr(),
                                                                mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
@@ -386,24 +395,35 @@ class _ResTail(torch.autograd.Function):
                 gy = gy.contiguous()
                 buf, _ = _bn_ws(B, C, H * W, y.device)
                 dil = 0
+                if syncbn.active() and not ctx.fold:
+                    # SyncBN: the partials first (all-reduced below), then the tail takes them (dil -1)
+                    _native.check(_native.load().honk_bn_partials_f32(
+                        gy.data_ptr(), y.data_ptr(), buf.data_ptr(), buf.numel(), B, C, H * W, st),
+                        "honk_bn_partials_f32")
+                    dil = -1
             if ctx.fold:
                 if dil == 0:
                     raise RuntimeError("honk_amd: a folded BatchNorm's gradient reached the tail without its conv")
-                _native.check(_native.load().honk_res_tail_bwd_mask_bn_f32(
-                    gy.data_ptr(), ptr(gs), y.data_ptr(), ctx.saved_tensors[3].data_ptr(), invstd.data_ptr(),
-                    h.data_ptr(), gh.data_ptr(), ptr(gold), B, C, H, W, dil, buf.data_ptr(), buf.numel(), st),
-                    "honk_res_tail_bwd_mask_bn_f32")
+                with _synced(buf):
+                    _native.check(_native.load().honk_res_tail_bwd_mask_bn_f32(
+                        gy.data_ptr(), ptr(gs), y.data_ptr(), ctx.saved_tensors[3].data_ptr(), invstd.data_ptr(),
+                        h.data_ptr(), gh.data_ptr(), ptr(gold), B, C, H, W, dil, buf.data_ptr(), buf.numel(), st),
+                        "honk_res_tail_bwd_mask_bn_f32")
             else:
-                _native.check(_native.load().honk_res_tail_bwd_mask_f32(
-                    gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(), h.data_ptr(), gh.data_ptr(), ptr(gold),
-                    B, C, H, W, dil, buf.data_ptr(), buf.numel(), st), "honk_res_tail_bwd_mask_f32")
+                with _synced(buf if dil != 0 else None):
+                    _native.check(_native.load().honk_res_tail_bwd_mask_f32(
+                        gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(), h.data_ptr(), gh.data_ptr(),
+                        ptr(gold), B, C, H, W, dil, buf.data_ptr(), buf.numel(), st), "honk_res_tail_bwd_mask_f32")
         elif pre is not None and pre[1] is gy and gy._version == pre[2]:
             # the statistics of exactly this gradient, summed by the conv that produced it
             STATS_USED["bwd"] += 1
-            _native.check(_native.load().honk_res_tail_bwd_part_f32(
-                gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(), h.data_ptr(), gh.data_ptr(), ptr(gold),
-                pre[0].data_ptr(), B, C, H, W, pre[3], st), "honk_res_tail_bwd_part_f32")
+            with _synced(pre[0]):
+                _native.check(_native.load().honk_res_tail_bwd_part_f32(
+                    gy.data_ptr(), ptr(gs), y.data_ptr(), invstd.data_ptr(), h.data_ptr(), gh.data_ptr(), ptr(gold),
+                    pre[0].data_ptr(), B, C, H, W, pre[3], st), "honk_res_tail_bwd_part_f32")
         else:
+            if syncbn.active():
+                raise RuntimeError("honk_amd: SyncBN needs the input-gradient conv's statistics on the unfused tail")
             gy = gy.contiguous()
             ws, nb = _bn_ws(B, C, H * W, y.device)
             _native.check(_native.load().honk_res_tail_bwd_f32(gy.data_ptr(), ptr(gs), y.data_ptr(),
@@ -411,6 +431,25 @@ class _ResTail(torch.autograd.Function):
                                                                ptr(gold), B, C, H * W, ws.data_ptr(), nb, st),
                           "honk_res_tail_bwd_f32")
         return gh, gold, None, None, None, None, None, None, None
+
+
+def _synced(buf):
+    """SyncBN (honk_amd.syncbn active): the partials in `buf` summed over the ranks, and
+    the native BatchNorm's element count scaled to the job's, around one tail call."""
+    if not syncbn.active():
+        return contextlib.nullcontext()
+    if buf is not None:
+        syncbn.allreduce_partials_(buf)
+    return syncbn.count_scaled()
+
+
+def stats_supported(x, d) -> bool:
+    """The fused tail of a conv of input x (dilation d) takes its BatchNorm statistics from
+    the conv epilogues (what SyncBN's native path needs)."""
+    if not (FUSE_TAIL and x.is_cuda and x.dim() == 4):
+        return False
+    B, C, H, W = x.shape
+    return int(_native.load().honk_conv3x3_stats_bytes(B, C, H, W, int(d))) > 0
 
 
 def res_tail(h, old, bn, keep_s=False, box=None, fold=False):
@@ -436,7 +475,10 @@ def bn_supported(x, bn) -> bool:
 
 def batch_norm_train(x, bn):
     """nn.BatchNorm2d.forward in training mode (affine=False, momentum set): the
-    module's num_batches_tracked bookkeeping, then the native normalisation."""
+    module's num_batches_tracked bookkeeping, then the native normalisation (SyncBN
+    active: honk_amd.syncbn.batch_norm, the ranks' statistics)."""
+    if syncbn.active():
+        return syncbn.batch_norm(x, bn)
     bn.num_batches_tracked.add_(1)
     y = _BatchNormTrain.apply(x, bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps))
     # the kernel updated the running stats through raw pointers: bump their version

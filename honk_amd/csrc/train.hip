@@ -2258,6 +2258,36 @@ extern "C" int honk_conv3x3_wgrad_bn_f32(const float* x, const float* dy, float*
   return conv3x3_wgrad(x, dy, dw, batch, c, h, w_, dil, fold_mean, fold_invstd, workspace, ws_bytes, stream);
 }
 
+// SyncBN (honk_amd/syncbn.py): the ranks' statistics partials are all-reduced before a
+// BatchNorm finalises them, and the element count is the whole job's -- this rank's times
+// the scale (the ranks' equal batches; thread-local, 1 outside a synchronised training)
+namespace {
+thread_local double g_bn_nscale = 1.0;
+double bn_count(int64_t batch, int64_t hw) { return (double)batch * (double)hw * g_bn_nscale; }
+}  // namespace
+
+extern "C" int honk_bn_count_scale(double k) {
+  if (!(k >= 1.0 && k <= 65536.0)) return fail(HONK_ERR_ARG, "BatchNorm count scale %g outside [1, 65536]", k);
+  g_bn_nscale = k;
+  return HONK_OK;
+}
+
+// The (sum a, sum a*b) partials of a BatchNorm statistic over [batch][c][hw] (b null: a*a)
+// into part ([c][S][2] doubles, S = the bn_slices count honk_bn_train_workspace_bytes sizes),
+// for a caller that reduces them itself (SyncBN: all-reduced across ranks, then handed to
+// honk_res_tail_bwd_mask*_f32 with dil = -1)
+extern "C" int honk_bn_partials_f32(const float* a, const float* b, void* part, size_t part_bytes, int64_t batch,
+                                    int32_t c, int64_t hw, void* stream) {
+  if (!a || !part) return fail(HONK_ERR_ARG, "null pointer argument");
+  if (batch < 1 || c < 1 || hw < 1 || hw > 0x7fffffff || batch > 0x7fffffff) return fail(HONK_ERR_ARG, "bad batchnorm shape");
+  const int S = train::bn_slices((int)batch, c);
+  if (part_bytes < (size_t)c * S * 2 * sizeof(double)) return fail(HONK_ERR_WORKSPACE, "partials buffer too small");
+  hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, (hipStream_t)stream, a, b, (double*)part,
+                     (int)batch, c, (int)hw, S);
+  HONK_LAUNCH_CHECK("bn_partial_kernel");
+  return HONK_OK;
+}
+
 extern "C" size_t honk_bn_train_workspace_bytes(int64_t batch, int32_t c, int64_t hw) {
   if (batch < 1 || c < 1 || hw < 1) return 0;
   return (size_t)c * train::bn_slices((int)batch, c) * 2 * sizeof(double) + (size_t)4 * c * sizeof(float);
@@ -2277,7 +2307,7 @@ extern "C" int honk_bn_train_fwd_f32(const float* x, float* y, float* mean, floa
                      (int)batch, c, (int)hw, S);
   HONK_LAUNCH_CHECK("bn_partial_kernel");
   hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, mean,
-                     invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
+                     invstd, running_mean, running_var, c, S, bn_count(batch, hw), momentum, eps);
   HONK_LAUNCH_CHECK("bn_stats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
@@ -2301,7 +2331,7 @@ extern "C" int honk_bn_train_bwd_f32(const float* dy, const float* y, const floa
   hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, dy, y, part, (int)batch, c, (int)hw, S);
   HONK_LAUNCH_CHECK("bn_partial_kernel");
   hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, m,
-                     m + c, c, S, (double)batch * (double)hw);
+                     m + c, c, S, bn_count(batch, hw));
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
@@ -2324,7 +2354,7 @@ extern "C" int honk_res_tail_fwd_f32(const float* h, const float* old, float* s,
   hipLaunchKernelGGL(train::tail_partial_kernel, dim3(c, S), dim3(256), 0, st, h, old, part, (int)batch, c, (int)hw, S);
   HONK_LAUNCH_CHECK("tail_partial_kernel");
   hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, mean,
-                     invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
+                     invstd, running_mean, running_var, c, S, bn_count(batch, hw), momentum, eps);
   HONK_LAUNCH_CHECK("bn_stats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
@@ -2348,7 +2378,7 @@ extern "C" int honk_res_tail_bwd_f32(const float* gy, const float* gs, const flo
   hipLaunchKernelGGL(train::bn_partial_kernel, dim3(c, S), dim3(256), 0, st, gy, y, part, (int)batch, c, (int)hw, S);
   HONK_LAUNCH_CHECK("bn_partial_kernel");
   hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, m,
-                     m + c, c, S, (double)batch * (double)hw);
+                     m + c, c, S, bn_count(batch, hw));
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
@@ -2482,7 +2512,7 @@ extern "C" int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, fl
   hipStream_t st = (hipStream_t)stream;
   const int64_t hw = (int64_t)hh * ww;
   hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)stats,
-                     mean, invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
+                     mean, invstd, running_mean, running_var, c, S, bn_count(batch, hw), momentum, eps);
   HONK_LAUNCH_CHECK("bn_stats_kernel");
   if (!y) return HONK_OK;  // the next conv folds the BatchNorm in (honk_conv3x3_tail_bn_f32)
   const int64_t total = batch * c * hw;
@@ -2499,7 +2529,7 @@ int res_tail_bwd_mask(const float* gy, const float* gs, const float* y, const fl
                       const uint32_t* mask, float* gh, float* gold, int64_t batch, int32_t c, int32_t hh, int32_t ww,
                       int32_t dil, void* stats, size_t stats_bytes, void* stream) {
   if (!gy || !y || !invstd || !mask || !gh || !stats) return fail(HONK_ERR_ARG, "null pointer argument");
-  if (ym && dil <= 0) return fail(HONK_ERR_UNSUPPORTED, "res tail: a folded BatchNorm needs the conv's statistics");
+  if (ym && dil == 0) return fail(HONK_ERR_UNSUPPORTED, "res tail: a folded BatchNorm needs the conv's statistics");
   if (batch < 1 || c < 1 || hh < 1 || ww < 1 || batch > 0x7fffffff || (int64_t)hh * ww > 0x7fffffff)
     return fail(HONK_ERR_ARG, "bad res tail shape");
   hipStream_t st = (hipStream_t)stream;
@@ -2512,6 +2542,10 @@ int res_tail_bwd_mask(const float* gy, const float* gs, const float* y, const fl
     if (stats_bytes < honk_conv3x3_stats_bytes(batch, c, hh, ww, dil))
       return fail(HONK_ERR_WORKSPACE, "statistics buffer %zu B < required %zu B", stats_bytes,
                   honk_conv3x3_stats_bytes(batch, c, hh, ww, dil));
+  } else if (dil < 0) {  // the caller's partials (honk_bn_partials_f32; SyncBN: all-reduced)
+    const size_t need = honk_bn_train_workspace_bytes(batch, c, hw);
+    if (stats_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", stats_bytes, need);
+    S = train::bn_slices((int)batch, c);
   } else {  // dil = 0: no conv consumed the gradient (the last block): sum them here
     const size_t need = honk_bn_train_workspace_bytes(batch, c, hw);
     if (stats_bytes < need) return fail(HONK_ERR_WORKSPACE, "workspace %zu B < required %zu B", stats_bytes, need);
@@ -2522,7 +2556,7 @@ int res_tail_bwd_mask(const float* gy, const float* gs, const float* y, const fl
   }
   float* m = (float*)(part + (size_t)c * S * 2);
   hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, m,
-                     m + c, c, S, (double)batch * (double)hw);
+                     m + c, c, S, bn_count(batch, hw));
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
@@ -2567,7 +2601,7 @@ extern "C" int honk_res_tail_fwd_part_f32(const float* h, const float* old, floa
   hipStream_t st = (hipStream_t)stream;
   const int64_t hw = (int64_t)hh * ww;
   hipLaunchKernelGGL(train::bn_stats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)stats,
-                     mean, invstd, running_mean, running_var, c, S, (double)batch * (double)hw, momentum, eps);
+                     mean, invstd, running_mean, running_var, c, S, bn_count(batch, hw), momentum, eps);
   HONK_LAUNCH_CHECK("bn_stats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;
@@ -2588,7 +2622,7 @@ extern "C" int honk_res_tail_bwd_part_f32(const float* gy, const float* gs, cons
   double* part = (double*)stats;
   float* m = (float*)(part + (size_t)c * S * 2);
   hipLaunchKernelGGL(train::bn_bstats_kernel, dim3((unsigned)c), dim3(256), 0, st, (const double*)part, m,
-                     m + c, c, S, (double)batch * (double)hw);
+                     m + c, c, S, bn_count(batch, hw));
   HONK_LAUNCH_CHECK("bn_bstats_kernel");
   const int64_t total = batch * c * hw;
   const int64_t nthr = (hw & 3) == 0 ? total / 4 : total;

@@ -39,6 +39,7 @@ from . import _native
 from . import cnn_train as _cnn_train
 from . import head_train as _head
 from . import conv3x3 as _conv3x3
+from . import syncbn as _syncbn
 
 
 class ConfigType(Enum):
@@ -214,7 +215,8 @@ class SpeechResModel(SerializableModule):
                 _conv3x3.warn_fallback(self, f"the block convs ({conv.weight.shape[0]} maps, "
                                              f"{tuple(x.shape[2:])} map, dilation {conv.dilation[0]})", phase)
             if native_convs and i > 0 and _conv3x3.supported(x, conv) and \
-                    _conv3x3.bn_supported(x, getattr(self, "bn{}".format(i))):
+                    _conv3x3.bn_supported(x, getattr(self, "bn{}".format(i))) and \
+                    (not _syncbn.active() or _conv3x3.stats_supported(x, conv.dilation[0])):
                 # conv, then relu / residual add / train BatchNorm as one fused tail
                 # statistics boxes: the tail's BatchNorm sums come from this conv's epilogue
                 # (forward) and from the next layer's input-gradient conv (backward)
@@ -262,7 +264,7 @@ class SpeechResModel(SerializableModule):
                 else:
                     if native_convs and bn.training:
                         _conv3x3.warn_fallback(self, "train-mode BatchNorm", phase)
-                    x = bn(x)
+                    x = _syncbn.batch_norm(x, bn) if (_syncbn.active() and bn.training) else bn(x)
         if native_convs and _head.supported(x):
             return _head.linear(_head.spatial_mean(x), self.output)
         x = x.view(x.size(0), x.size(1), -1)  # shape: (batch, feats, o3)

@@ -27,6 +27,7 @@ import torch.nn as nn
 import torch.utils.data as data
 
 from . import distributed as hd
+from . import syncbn
 from . import head_train
 from .data import batch_input
 from . import model as mod
@@ -147,7 +148,9 @@ def train(config, datasets=None):
     broadcast of the flat buffer bucket per step), the gradient bucket is summed
     with ONE all-reduce -- started from the hook of the last gradient backward
     writes -- and averaged in the SGD kernel: two collectives per step.  Only rank
-    0 prints and saves.
+    0 prints and saves.  ``sync_bn`` (or HONK_SYNC_BN=1): SyncBN instead of the
+    per-replica statistics, one more all-reduce per BatchNorm and direction
+    (honk_amd/syncbn.py).
     """
     rank, world = hd.world_info()
     log = rank == 0
@@ -182,11 +185,18 @@ def train(config, datasets=None):
     dev_loader = data.DataLoader(dev_set, batch_size=min(len(dev_set), 16), shuffle=False,
                                  collate_fn=getattr(dev_set, "collate_fn", None))
     test_loader = _whole_set_loader(test_set)
+    # optional SyncBN (config["sync_bn"] or HONK_SYNC_BN=1; honk_amd/syncbn.py): the
+    # train-mode BatchNorms normalise with the whole job's statistics instead of the shard's
+    sync = world > 1 and bool(config.get("sync_bn", os.environ.get("HONK_SYNC_BN", "0") == "1"))
+    if sync:
+        syncbn.enable()
     try:
         best_model = _train_epochs(config, model, train_set, dev_set, train_loader, dev_loader, sampler, flat,
                                    fbuf, reducer, optimizer, schedule_steps, criterion, log)
     finally:
         reducer.remove()  # no gradient hooks (and no stray all-reduce) outlive train()
+        if sync:
+            syncbn.disable()
     if log:
         evaluate(config, best_model, test_loader)
 

@@ -302,6 +302,18 @@ int honk_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, int64_t b
  * dx = invstd * (dy - mean(dy) - y * mean(dy * y)).  NCHW fp32, hw = H * W.
  */
 size_t honk_bn_train_workspace_bytes(int64_t batch, int32_t c, int64_t hw);
+/*
+ * SyncBN (optional; honk_amd/syncbn.py): the caller all-reduces every
+ * statistics-partials buffer across the data-parallel ranks before the BatchNorm that
+ * finalises it, and sets the element-count scale k (the ranks' equal batches: k = world
+ * size; thread-local, 1 by default) so the mean / variance / running statistics are the
+ * whole job's.  honk_bn_partials_f32 writes the (sum a, sum a*b) partials ([c][S][2]
+ * doubles, b NULL: a*a; S as honk_bn_train_workspace_bytes sizes) for a caller that reduces
+ * them itself; honk_res_tail_bwd_mask*_f32 takes them with dil = -1.
+ */
+int honk_bn_count_scale(double k);
+int honk_bn_partials_f32(const float* a, const float* b, void* part, size_t part_bytes, int64_t batch, int32_t c,
+                         int64_t hw, void* stream);
 int honk_bn_train_fwd_f32(const float* x, float* y, float* mean, float* invstd, float* running_mean,
                           float* running_var, int64_t batch, int32_t c, int64_t hw, float momentum, float eps,
                           void* workspace, size_t workspace_bytes, void* stream);
@@ -357,7 +369,8 @@ int honk_res_tail_fwd_s_f32(const float* s, float* y, float* mean, float* invstd
                             int32_t dil, float momentum, float eps, void* stream);
 /* dil >= 1: `stats` = the input-gradient conv's partials (honk_conv3x3_stats_f32 mode 2 at
  * dilation dil); dil = 0: `stats` is a workspace of honk_bn_train_workspace_bytes(batch, c,
- * hh * ww) and the statistics are summed here (a block whose output feeds no conv). */
+ * hh * ww) and the statistics are summed here (a block whose output feeds no conv);
+ * dil = -1: that workspace already holds honk_bn_partials_f32(gy, y) (SyncBN). */
 int honk_res_tail_bwd_mask_f32(const float* gy, const float* gs, const float* y, const float* invstd,
                                const uint32_t* mask, float* gh, float* gold, int64_t batch, int32_t c,
                                int32_t hh, int32_t ww, int32_t dil, void* stats, size_t stats_bytes, void* stream);
