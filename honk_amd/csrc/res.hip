@@ -1455,8 +1455,9 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   // stream pixels stay at a constant LDS pitch across a row change
   pp.slotb = (int)(W * PXB + ((pp.ppr * 1024 - W * PXB + 255) / 256) * 256);
   if (lin) pp.slotb = (int)(W * PXB);  // rows contiguous in the ring (block16p_body LIN)
-  if (FM == 2 && padcols) {
-    // f16x2 last layer (res_bf16p.inc PADC): zero columns either side of every slot's
+  if ((FM == 2 || FM == 0) && padcols) {
+    // the tap-step instances and the last layer on the row table (res_bf16p.inc PADC; f16x2,
+    // and bf16's: its one-stream pairs and res15's last layer): zero columns either side of every slot's
     // row, at least the widest tap offset (B's sB d columns), in 256-B units; the DMA's
     // pieces and their zero tail after the left pad
     const long sc = (long)sB * d;
@@ -1628,7 +1629,8 @@ static PairPlan last_at(const Layout& L, const honk_res_desc* d, int FM, int i) 
   pp.NRB = 1;
   pp.lag = 0;
   pp.ns = ns;
-  pp.ok = (long)(pp.NRA + 1) * pp.slotb + g16p_lds_extra(FM == 2, 2, pp.slotb) <= g16p_lds_bytes() / ns;
+  pp.ok = (long)(pp.NRA + 1) * pp.slotb + g16p_lds_extra(FM == 2 || (FM == 0 && pp.padb > 0), 2, pp.slotb) <=
+          g16p_lds_bytes() / ns;
   return pp.ok ? pp : no;
 }
 

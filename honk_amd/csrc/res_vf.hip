@@ -69,6 +69,8 @@ bool launch_pairk_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Blo
 void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
   if (FM == 1) hipLaunchKernelGGL((block16l_kernel<3, 2, 9, 9, 2>), gd, bd, 0, st, pa);
   else if (FM == 2 && d == 16) hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2, 2, 16>), gd, bd, 0, st, pa);
+  // bf16, res15's last layer: the row table with pad columns and the compile-time tap step
+  else if (FM == 0 && d == 16 && pa.padb > 0) hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2, 0, 16>), gd, bd, 0, st, pa);
   else if (FM == 2) hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2, 2>), gd, bd, 0, st, pa);
   else hipLaunchKernelGGL((block16l_kernel<3, 1, 4, 4, 2>), gd, bd, 0, st, pa);
 }

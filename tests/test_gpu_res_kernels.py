@@ -235,6 +235,22 @@ def test_last_kernel_vs_w(monkeypatch, name, override, B, prec):
         assert np.abs(outl[idx] - ref).max() <= 0.05
 
 
+@pytest.mark.parametrize("B", [600, 7])
+def test_bf16_single_stream_tap_step_pairs_bitwise(monkeypatch, B):
+    """bf16 pairs on one stream per workgroup (HONK_PAIR_STREAMS=1: the compile-time
+    tap-step instances, block16p_kernel<3, 1, 4, 4, 1, 0, dA, dB>, rings with zero pad
+    columns -- also what a 40-pixel-row model takes when two streams do not fit the LDS)
+    compute what the default two-stream row-table pairs compute, bit for bit."""
+    cfg = dict(ref_configs()["res15"])
+    params, x = _case(cfg, B, seed=53)
+    m = _module(cfg, params, "res15", "bf16")
+    monkeypatch.delenv("HONK_PAIR_STREAMS", raising=False)
+    out2 = _run(m, x)
+    monkeypatch.setenv("HONK_PAIR_STREAMS", "1")
+    out1 = _run(m, x)
+    assert np.array_equal(out1, out2), float(np.abs(out1 - out2).max())
+
+
 @pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
 def test_last_kernel_batch_invariance(monkeypatch, prec):
     """Several clips per workgroup stream at different positions: a clip's logits do
