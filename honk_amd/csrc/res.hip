@@ -1591,6 +1591,14 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
       const PairPlan pl = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, false, true, 1, true);
       if (pl.ok && pl.ppr == 2 && pl.ppw <= 4) return pl;
     }
+    // 40-pixel rows: the compile-time tap-step instances where their pad columns fit two
+    // streams (res15's (1,1) (1,2) (2,2) (4,4) pairs; HONK_PAIR_IMM2=0 keeps the row table)
+    const char* ie = getenv("HONK_PAIR_IMM2");
+    if (pair_imm(L, FM, dA, dB) && !(ie && ie[0] == '0')) {
+      PairPlan pi = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, true, true);
+      pi.tbl = false;
+      if (pi.ok && pi.ppr == 4 && pi.ppw <= pair_ppw(SP, pi.ppr)) return pi;
+    }
     const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, false, true);
     if (p2.ok && (p2.ppr == 4 || p2.ppr == 2) && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
   }
@@ -1846,6 +1854,7 @@ bool launch_pair_vf(int FM, int ppr, bool imm, int dA, int dB, dim3 gd, dim3 bd,
                     const Block16PArgs& pa);
 void launch_last_vf(int FM, int d, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 void launch_pair2t_vf(int ppr, bool lin, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
+bool launch_pair2i_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 bool launch_pairk_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa);
 
 // flags (f16x2 only, may be null): [batch] the clips' admission flags (clip_scale_kernel,
@@ -1941,6 +1950,10 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             if (pp.ks == 2) {
               if (!launch_pairk_vf(dA, dil_of(d, i + 1), gd, bd, st, pa))
                 return fail(HONK_ERR_UNSUPPORTED, "block16k: no instance for dilations %d, %d", dA, dil_of(d, i + 1));
+            } else if (FM == 0 && pp.ns == 2 && pp.padb > 0) {
+              if (!launch_pair2i_vf(dA, dil_of(d, i + 1), gd, bd, st, pa))
+                return fail(HONK_ERR_UNSUPPORTED, "block16p: no two-stream tap-step instance for dilations %d, %d", dA,
+                            dil_of(d, i + 1));
             } else if (FM == 0 && pp.ns == 2) launch_pair2t_vf(pp.ppr, pp.lin, gd, bd, st, pa);
             else if (!launch_pair_vf(FM, pp.ppr, pp.ppr == 4 && pp.padb > 0, dA, dil_of(d, i + 1), gd, bd, st, pa))
               return fail(HONK_ERR_UNSUPPORTED, "block16p: no tap-step instance for dilations %d, %d", dA,

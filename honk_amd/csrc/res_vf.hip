@@ -53,6 +53,19 @@ void launch_pair2t_vf(int ppr, bool lin, dim3 gd, dim3 bd, hipStream_t st, const
   else hipLaunchKernelGGL((block16p_kernel<3, 1, 2, 5, 2, 0, -1, -1>), gd, bd, 0, st, pa);
 }
 
+// bf16, two streams on the compile-time tap-step instances (rings with zero pad columns,
+// where those fit two streams: res15's (1,1) (1,2) (2,2) (4,4) pairs)
+bool launch_pair2i_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
+#define HONK_P2I(a_, b_)                                                              \
+  if (dA == a_ && dB == b_) {                                                         \
+    hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2, 0, a_, b_>), gd, bd, 0, st, pa); \
+    return true;                                                                      \
+  }
+  HONK_P2I(1, 1) HONK_P2I(1, 2) HONK_P2I(2, 2) HONK_P2I(4, 4)
+#undef HONK_P2I
+  return false;
+}
+
 // f16x2 with the contraction split over two waves per SIMD (res_bf16k.inc)
 bool launch_pairk_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
 #define HONK_PK(a_, b_)                                                       \
