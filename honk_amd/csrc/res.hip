@@ -1409,6 +1409,7 @@ struct PairPlan {
   bool tbl;                            // bf16 two streams: the row-table instance (SCA = -1)
   int ks;                              // 2: f16x2 with K split over two waves per SIMD (block16k_kernel)
   bool lin;                            // bf16 two streams, undilated A: linear A-in DMA (block16p_body LIN)
+  int ringpad;                         // shared pad columns (Block16PArgs::ringpad)
 };
 static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t n, int grid, int i);
 static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
@@ -1445,8 +1446,8 @@ static bool use_w_kernel(const Layout& L, const honk_res_desc* d, int FM) {
 // class rows), at most `cpw` clips per workgroup: B's lag and the ring sizes from
 // an exact walk over the steps of the longest stream.  ok = false: does not fit.
 static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int nstreams = 1, bool padcols = false,
-                          bool tbl = false, int ks = 1, bool lin = false) {
-  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams, tbl, ks, lin};
+                          bool tbl = false, int ks = 1, bool lin = false, bool sharedpad = false) {
+  PairPlan pp{false, 0, 0, 0, 0, 0, 0, 0, nstreams, tbl, ks, lin, 0};
   const int SP = sp_of(FM);
   const int P = 64, W = L.W, H = L.H;
   const long PXB = g16p_pxb(L.NT, SP);  // LDS pixel pitch
@@ -1464,6 +1465,13 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
     pp.padb = (int)((sc * PXB + 255) / 256 * 256);
     const long right = W * PXB + pp.padb > pp.ppr * 1024L ? W * PXB + pp.padb : pp.ppr * 1024L;
     pp.slotb = (int)((pp.padb + right + 255) / 256 * 256);
+    // shared pads: a slot = its left pad + the row, the right pad being the next slot's left
+    // pad (zero too: the DMA's tail zeros land there, hence padb >= the piece tail, 256 B),
+    // one more pad after ring B (plan ringpad; ring A's last slot reads ring B's first left pad)
+    if (sharedpad && pp.padb >= 256 && (W * PXB) % 256 == 0 && pp.ppr * 1024 - W * PXB <= pp.padb) {
+      pp.slotb = (int)(pp.padb + W * PXB);
+      pp.ringpad = pp.padb;
+    }
   }
   const long total = (long)cpw * H * W, rows_total = (long)cpw * H;
   if (total >= (1L << 24) || sB < 1 || sB > 2) return pp;
@@ -1541,9 +1549,10 @@ static PairPlan plan_pair(const Layout& L, int FM, int d, int sB, int cpw, int n
   const long extra = ks == 2 ? g16p_lds_extra(true, 8, pp.slotb) + g16k_xch_bytes()
                              : g16p_lds_extra(FM == 2 || padcols || tbl, 4, pp.slotb);
   if (tbl && nstreams > 1)  // the streams share the zero block, sink and zeroed slot (block16p_body SHZ)
-    pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + 4 * g16p_tr() * g16p_teb() <= g16p_stream_bytes(nstreams, pp.slotb);
+    pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + pp.ringpad + 4 * g16p_tr() * g16p_teb() <=
+            g16p_stream_bytes(nstreams, pp.slotb + pp.ringpad);
   else
-    pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + extra <= g16p_lds_bytes() / nstreams;
+    pp.ok = (long)(pp.NRA + pp.NRB) * pp.slotb + 2L * pp.ringpad + extra <= g16p_lds_bytes() / nstreams;
   return pp;
 }
 
@@ -1598,6 +1607,10 @@ static PairPlan pair_at(const Layout& L, const honk_res_desc* d, int FM, int64_t
       PairPlan pi = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, true, true);
       pi.tbl = false;
       if (pi.ok && pi.ppr == 4 && pi.ppw <= pair_ppw(SP, pi.ppr)) return pi;
+      // the pads shared between neighbouring slots (one pad per slot): (8,8) then fits
+      pi = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, true, true, 1, false, true);
+      pi.tbl = false;
+      if (pi.ok && pi.ringpad > 0 && pi.ppr == 4 && pi.ppw <= pair_ppw(SP, pi.ppr)) return pi;
     }
     const PairPlan p2 = plan_pair(L, FM, dA, sB, (int)cdiv(cdiv(n, grid), 2), 2, false, true);
     if (p2.ok && (p2.ppr == 4 || p2.ppr == 2) && p2.ppw <= pair_ppw(SP, p2.ppr)) return p2;
@@ -1945,6 +1958,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.slotb = pp.slotb;
             pa.ppr = pp.ppr;
             pa.padb = pp.padb;
+            pa.ringpad = pp.ringpad;
             TimedLaunch tl(st, 2.0 * layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(256 * pp.ns * pp.ks);
             if (pp.ks == 2) {
@@ -1982,6 +1996,7 @@ static int forward_bf16(const Layout& L, const honk_res_desc* d, const float* pa
             pa.slotb = lp.slotb;
             pa.ppr = lp.ppr;
             pa.padb = lp.padb;
+            pa.ringpad = lp.ringpad;
             pa.chsum = chsum;
             TimedLaunch tl(st, layer_flop_per_clip * (double)n);
             const dim3 gd(grid), bd(128 * lp.ns);

@@ -54,14 +54,15 @@ void launch_pair2t_vf(int ppr, bool lin, dim3 gd, dim3 bd, hipStream_t st, const
 }
 
 // bf16, two streams on the compile-time tap-step instances (rings with zero pad columns,
-// where those fit two streams: res15's (1,1) (1,2) (2,2) (4,4) pairs)
+// where those fit two streams: res15's (1,1) (1,2) (2,2) (4,4) pairs, (8,8) with shared pads;
+// (4,8) needs 17 ring slots, 4.6 KiB past half the LDS, and stays on the row table)
 bool launch_pair2i_vf(int dA, int dB, dim3 gd, dim3 bd, hipStream_t st, const Block16PArgs& pa) {
 #define HONK_P2I(a_, b_)                                                              \
   if (dA == a_ && dB == b_) {                                                         \
     hipLaunchKernelGGL((block16p_kernel<3, 1, 4, 4, 2, 0, a_, b_>), gd, bd, 0, st, pa); \
     return true;                                                                      \
   }
-  HONK_P2I(1, 1) HONK_P2I(1, 2) HONK_P2I(2, 2) HONK_P2I(4, 4)
+  HONK_P2I(1, 1) HONK_P2I(1, 2) HONK_P2I(2, 2) HONK_P2I(4, 4) HONK_P2I(8, 8)
 #undef HONK_P2I
   return false;
 }

@@ -240,15 +240,22 @@ def test_bf16_single_stream_tap_step_pairs_bitwise(monkeypatch, B):
     """bf16 pairs on one stream per workgroup (HONK_PAIR_STREAMS=1: the compile-time
     tap-step instances, block16p_kernel<3, 1, 4, 4, 1, 0, dA, dB>, rings with zero pad
     columns -- also what a 40-pixel-row model takes when two streams do not fit the LDS)
-    compute what the default two-stream row-table pairs compute, bit for bit."""
+    compute what the default two-stream pairs compute (the tap-step instances where their pads
+    fit two streams, (8,8) with pads shared between neighbouring slots; the row table for
+    (4,8)), and what the two-stream row-table pairs compute (HONK_PAIR_IMM2=0), bit for bit."""
     cfg = dict(ref_configs()["res15"])
     params, x = _case(cfg, B, seed=53)
     m = _module(cfg, params, "res15", "bf16")
     monkeypatch.delenv("HONK_PAIR_STREAMS", raising=False)
+    monkeypatch.delenv("HONK_PAIR_IMM2", raising=False)
     out2 = _run(m, x)
+    monkeypatch.setenv("HONK_PAIR_IMM2", "0")
+    outt = _run(m, x)
+    monkeypatch.delenv("HONK_PAIR_IMM2")
     monkeypatch.setenv("HONK_PAIR_STREAMS", "1")
     out1 = _run(m, x)
     assert np.array_equal(out1, out2), float(np.abs(out1 - out2).max())
+    assert np.array_equal(outt, out2), float(np.abs(outt - out2).max())
 
 
 @pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
