@@ -291,7 +291,7 @@ def _res_geometry(cfg):
     return 101 // ph, 40 // pw, int(cfg["n_layers"]), 16 * ((C + 15) // 16)
 
 
-def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
+def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan, steps=None):
     """Roofline of the res block convs (the dilated 3x3 layers) for a precision mode.
 
     MFMA-bound: achieved = ALGORITHMIC flop (2 x 9 x C^2 x H x W per
@@ -307,8 +307,10 @@ def res_roofline(prec, cfg, kms, nl, kfl, B, model, plan):
     H, W, L, CP = _res_geometry(cfg)
     ach = kfl / (kms * 1e-3) / 1e12 if nl and kms else None
     peak = MODE_PEAK[prec]
-    clips = min(B, 4096)
     chunk_fwds = nl / max(len(plan), 1)
+    # clips per chunk (the library's chunk_clips: 4096, 8192 for pooled maps): the timed
+    # clips over the chunk forwards the timed launches make up
+    clips = int(round(B * steps / chunk_fwds)) if steps and chunk_fwds else min(B, 4096)
     if prec == "f32":
         act = H * W * CP * 4
         per_clip = sum(act * (1 + (1 if i % 2 == 0 else 0) + (1 if i < L else 0)) for i in range(1, L + 1))
@@ -530,7 +532,7 @@ def measure_res(ctx, args, name, prec, B, x=None, model=None):
     return {"value": round(ctx.world * B * args.steps / el, 1), "unit": "clips/s", "dtype": prec,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "per_rank_clips_s": [round(B * args.steps / t, 1) for t in per],
-            "roofline": res_roofline(prec, cfg, kms, nl, kfl, B, name, plan),
+            "roofline": res_roofline(prec, cfg, kms, nl, kfl, B, name, plan, args.steps),
             "parity": _sample_parity(model, cfg, x, out, orc, B),
             "note": PREC_NOTES[prec]}
 
@@ -771,7 +773,7 @@ def rank_main(args):
     flop_clip = orc.flops_per_clip(cfg)
     if is_res:
         roof = res_roofline(prec, cfg, kms, nlaunch, kflop, B, args.model,
-                            ctx.native.res_launch_plan(model._desc(101, 40, prec), B))
+                            ctx.native.res_launch_plan(model._desc(101, 40, prec), B), args.steps)
     else:
         avg_ms = kms / max(nlaunch, 1)
         ach = (kflop / max(nlaunch, 1)) / (avg_ms * 1e-3) / 1e12 if nlaunch else None

@@ -1285,8 +1285,13 @@ static int make_layout(const honk_res_desc* d, Layout* L) {
 
 static int64_t chunk_clips(const Layout& L, int64_t batch) {
   const size_t per_clip = (size_t)L.H * L.W * L.CP * sizeof(float);
-  // 4096 clips (3.2 GB per buffer for res15) keeps >200 tiles per CU per launch
-  int64_t ch = per_clip <= ((size_t)1 << 20) ? 4096 : (int64_t)((size_t)4 << 30) / (int64_t)per_clip;
+  // 4096 clips (3.2 GB per buffer for res15) keeps >200 tiles per CU per launch; pooled maps
+  // (res8 25 x 13, res26 50 x 20: <= 256 KiB per clip) take 8192 -- a res8 chunk's six
+  // launches are ~0.45 ms at 4096 clips, and C3 measured 9.40M -> 10.07M clips/s at 8192
+  // (16384 / 32768 within 0.5 % of it; res15 unchanged at 8192; exp/chunk_ab.sh)
+  int64_t ch = per_clip <= ((size_t)256 << 10)   ? 8192
+               : per_clip <= ((size_t)1 << 20) ? 4096
+                                               : (int64_t)((size_t)4 << 30) / (int64_t)per_clip;
   if (const char* e = getenv("HONK_RES_CHUNK")) ch = atoll(e);
   if (ch < 1) ch = 1;
   return batch < ch ? batch : ch;

@@ -3,7 +3,7 @@
 # bench's secondary configs, so every roofline sub-object carries a PMC traffic:
 #   c2f  cnn-trad-pool2 f32      (65,536 clips per step)
 #   c2x  cnn-trad-pool2 bf16x3
-#   c3   res8 bf16               (4096-clip chunks)
+#   c3   res8 bf16               (8192-clip chunks, two per step)
 #   c5   res26-narrow training   (4096 clips, 1 warmup + 1 timed step)
 # then on the CPU side:  python tools/pmc_summary.py gpurun_out/prof <tag>_c2f 65536 cnn-trad-pool2  (etc.)
 set -e
