@@ -10,7 +10,7 @@ OUT=$ROOT/exp/_var; mkdir -p "$OUT"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -I "$ROOT/include" \
   ${HONK_VFLAGS} -c "$SRC/$FILE.hip" -o "$OUT/${FILE}_$NAME.o"
 OBJS=""
-for f in runtime res cnn train mfcc head augment; do
+for f in runtime res res_vf cnn train mfcc head augment; do
   if [ "$f" = "$FILE" ]; then OBJS="$OBJS $OUT/${FILE}_$NAME.o"; else OBJS="$OBJS $ROOT/honk_amd/_build/$f.o"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libhonk_$NAME.so" $OBJS

@@ -605,6 +605,39 @@ __global__ __launch_bounds__(256) void tail_sum_kernel(const float* __restrict__
 #include "res_bf16k.inc"
 #include "res_bf16n.inc"
 
+// conv0m / conv0p staging: the clip's [Hin][Win] fp32 map through put(r, c, v), 256 threads.
+// Rows of whole float4s: a thread's U loads all in flight before its first LDS write (res8 /
+// res15: 1010 float4s, 4 per thread -- one HBM latency per clip instead of four in series).
+template <typename Put>
+__device__ __forceinline__ void c0_stage(const float* __restrict__ xc, int Hin, int Win, Put&& put) {
+  if ((Win & 3) == 0) {
+    constexpr int U = 4;
+    const int w4 = Win >> 2, n4 = Hin * w4;
+    for (int i0 = threadIdx.x; i0 < n4; i0 += U * 256) {
+      f32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * 256;
+        v[u] = i < n4 ? *(const f32x4*)(xc + 4 * (size_t)i) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * 256;
+        if (i < n4) {
+          const int r = i / w4, c = (i - r * w4) * 4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) put(r, c + e, v[u][e]);
+        }
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < Hin * Win; i += 256) {
+      const int r = i / Win;
+      put(r, i - r * Win, xc[i]);
+    }
+  }
+}
+
 // --------------------------------------------------------------------------- //
 // conv0 on the matrix cores (the bf16 / bf16x3 / f16x2 paths): 1 -> CP 3x3 pad 1,
 // ReLU, avg-pool PH x PW (model.py:87-89, 107-110), written in the block
@@ -692,20 +725,7 @@ __global__ __launch_bounds__(256, 7) void conv0m_kernel(const float* __restrict_
     hp[i] = __builtin_bit_cast(unsigned short, h);
     lp[i] = __builtin_bit_cast(unsigned short, (__bf16)(v - (float)h));
   };
-  if ((Win & 3) == 0) {
-    const int w4 = Win >> 2, n4 = Hin * w4;
-    for (int i = threadIdx.x; i < n4; i += 256) {
-      const int r = i / w4, c = (i - r * w4) * 4;
-      const f32x4 v = *(const f32x4*)(xc + (size_t)r * Win + c);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) put(r, c + u, v[u]);
-    }
-  } else {
-    for (int i = threadIdx.x; i < Hin * Win; i += 256) {
-      const int r = i / Win;
-      put(r, i - r * Win, xc[i]);
-    }
-  }
+  c0_stage(xc, Hin, Win, put);
   __syncthreads();
 
   const int npo = H * W;                 // pooled outputs
@@ -844,20 +864,7 @@ __global__ __launch_bounds__(256, 5) void conv0p_kernel(const float* __restrict_
     hp[i] = __builtin_bit_cast(unsigned short, h);
     lp[i] = __builtin_bit_cast(unsigned short, (__bf16)(v - (float)h));
   };
-  if ((Win & 3) == 0) {
-    const int w4 = Win >> 2, n4 = Hin * w4;
-    for (int i = threadIdx.x; i < n4; i += 256) {
-      const int r = i / w4, c = (i - r * w4) * 4;
-      const f32x4 v = *(const f32x4*)(xc + (size_t)r * Win + c);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) put(r, c + u, v[u]);
-    }
-  } else {
-    for (int i = threadIdx.x; i < Hin * Win; i += 256) {
-      const int r = i / Win;
-      put(r, i - r * Win, xc[i]);
-    }
-  }
+  c0_stage(xc, Hin, Win, put);
   __syncthreads();
 
   const int npo = H * W;
